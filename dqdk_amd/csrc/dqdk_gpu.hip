@@ -1,0 +1,496 @@
+/*
+ * dqdk_gpu.hip -- host runtime behind the C ABI in include/dqdk_gpu.h.
+ *
+ * One dqdk_gpu_queue per RX queue (the reference's dqdk_worker_t,
+ * src/dqdk.h:87-105): a HIP stream, the queue's device histogram (the
+ * per-GPU partial of tristan_t::histo, src/tristan.h:86), cumulative
+ * counters (dqdk_stats_t + tristan_t atomics) and per-batch scratch.
+ * Every batch is three short launches on the queue stream; nothing is
+ * computed on the host.
+ */
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rx_kernels.h"
+
+using namespace dqdk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* what, hipError_t e)
+{
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return -EIO;
+}
+
+int fail_errno(int err, const char* what)
+{
+    g_err = what;
+    return err;
+}
+
+#define HIPCHK(x)                           \
+    do {                                    \
+        hipError_t e_ = (x);                \
+        if (e_ != hipSuccess)               \
+            return fail(#x, e_);            \
+    } while (0)
+
+constexpr int kStages = 3;
+constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
+
+uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
+{
+    switch (mode) {
+    case DQDK_MODE_LISTMODE:
+    case DQDK_MODE_ENERGYHISTO:
+        return payloadsz / 16;
+    case DQDK_MODE_LISTWAVE:
+    case DQDK_MODE_WAVEFORM:
+        return 1;
+    default:
+        return 0;
+    }
+}
+
+struct Reg {
+    void* host;
+    uint64_t size;
+    void* dev;
+};
+
+}  // namespace
+
+struct dqdk_gpu_queue {
+    int device = 0;
+    dqdk_gpu_cfg_t cfg{};
+    uint32_t E = 0;
+    uint32_t max_batch = 0;
+    int histo = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    uint32_t* d_hist = nullptr;
+    dqdk_gpu_counters_t* d_cum = nullptr;
+    uint64_t* d_batch = nullptr;
+    uint32_t* d_keys = nullptr;
+    dqdk_gpu_desc_t* d_desc = nullptr;
+    dqdk_gpu_rx_result_t* d_res = nullptr;
+    std::vector<Reg> regs;
+    // stage timing
+    int timing = 0;
+    std::vector<hipEvent_t> ev_free;
+    struct Pending {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    double stage_ms[kStages] = {0, 0, 0};
+    uint64_t counts[kStages] = {0, 0, 0};
+};
+
+namespace {
+
+int ev_get(dqdk_gpu_queue* q, hipEvent_t* e)
+{
+    if (!q->ev_free.empty()) {
+        *e = q->ev_free.back();
+        q->ev_free.pop_back();
+        return 0;
+    }
+    HIPCHK(hipEventCreate(e));
+    return 0;
+}
+
+struct StageTimer {
+    dqdk_gpu_queue* q;
+    int stage;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageTimer(dqdk_gpu_queue* q_, int s) : q(q_), stage(s)
+    {
+        if (q->timing && ev_get(q, &a) == 0 && ev_get(q, &b) == 0)
+            (void)hipEventRecord(a, q->stream);
+    }
+    ~StageTimer()
+    {
+        if (q->timing && a && b) {
+            (void)hipEventRecord(b, q->stream);
+            q->pending.push_back({stage, a, b});
+        }
+    }
+};
+
+int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
+                 uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
+{
+    uint32_t* keys = d_keys ? d_keys : q->d_keys;
+    if (q->histo && q->E && !keys)
+        return fail_errno(-EINVAL, "histogram mode needs a key buffer");
+
+    RxArgs ra{};
+    ra.umem = d_umem;
+    ra.umem_size = umem_size;
+    ra.desc = d_desc;
+    ra.n = n;
+    ra.res = d_res;
+    ra.keys = keys;
+    ra.E = q->E;
+    ra.flags = q->cfg.flags;
+    ra.port_start = q->cfg.port_start;
+    ra.port_end = q->cfg.port_end;
+    ra.batch_scratch = q->d_batch;
+
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    const uint32_t grid_dec = std::min<uint32_t>(ntiles, (uint32_t)q->cu_count * 8u);
+    {
+        StageTimer t(q, 0);
+        hipLaunchKernelGGL(rx_decode_kernel, dim3(grid_dec), dim3(kTile), 0, q->stream, ra);
+        HIPCHK(hipGetLastError());
+    }
+
+    CountArgs ca{};
+    ca.res = d_res;
+    ca.n = n;
+    ca.E = q->E;
+    ca.flags = q->cfg.flags;
+    ca.histo = q->histo;
+    ca.batch_scratch = q->d_batch;
+    ca.cum = q->d_cum;
+    const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
+    {
+        StageTimer t(q, 1);
+        hipLaunchKernelGGL(rx_abort_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
+        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
+        HIPCHK(hipGetLastError());
+    }
+
+    if (q->histo && q->E) {
+        HistoArgs ha{};
+        ha.res = d_res;
+        ha.keys = keys;
+        ha.n = n;
+        ha.E = q->E;
+        ha.flags = q->cfg.flags;
+        ha.batch_scratch = q->d_batch;
+        ha.hist = q->d_hist;
+        const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
+        StageTimer t(q, 2);
+        hipLaunchKernelGGL(rx_histo_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
+        HIPCHK(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dqdk_gpu_abi_version(void) { return DQDK_GPU_ABI_VERSION; }
+
+const char* dqdk_gpu_last_error(void) { return g_err.c_str(); }
+
+int dqdk_gpu_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_batch, dqdk_gpu_queue_t** out)
+{
+    if (!cfg || !out || max_batch == 0)
+        return fail_errno(-EINVAL, "queue_create: bad argument");
+    *out = nullptr;
+    if (cfg->mode > DQDK_MODE_ENERGYHISTO || cfg->payloadsz > (16u << 20))
+        return fail_errno(-EINVAL, "queue_create: bad mode or payloadsz");
+    int ndev = dqdk_gpu_device_count();
+    if (device < 0 || device >= ndev)
+        return fail_errno(-ENODEV, "queue_create: no such HIP device");
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail_errno(-ENODEV, "queue_create: device is not gfx950 (MI355X)");
+    HIPCHK(hipSetDevice(device));
+
+    dqdk_gpu_queue* q = new dqdk_gpu_queue();
+    q->device = device;
+    q->cfg = *cfg;
+    q->E = events_per_payload(cfg->mode, cfg->payloadsz);
+    q->max_batch = max_batch;
+    q->histo = !(cfg->flags & DQDK_GPU_F_NO_HISTO) &&
+               (cfg->mode == DQDK_MODE_LISTWAVE || cfg->mode == DQDK_MODE_LISTMODE ||
+                cfg->mode == DQDK_MODE_ENERGYHISTO);  // is_store_histo, src/tristan.c:65-70
+    q->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+
+    auto cleanup = [&](int rc) {
+        dqdk_gpu_queue_destroy(q);
+        return rc;
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&q->own_stream, hipStreamNonBlocking)) != hipSuccess)
+        return cleanup(fail("hipStreamCreate", e));
+    q->stream = q->own_stream;
+    if ((e = hipMalloc(&q->d_cum, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
+        (e = hipMalloc(&q->d_batch, kBatchScratch * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMalloc(&q->d_desc, (size_t)max_batch * sizeof(dqdk_gpu_desc_t))) != hipSuccess ||
+        (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess)
+        return cleanup((fail("hipMalloc", e), -ENOMEM));
+    if ((e = hipMemset(q->d_cum, 0, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
+        (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
+        return cleanup(fail("hipMemset", e));
+    if (q->histo) {
+        if ((e = hipMalloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
+            return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
+        if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
+            return cleanup(fail("hipMemset(histogram)", e));
+        if (q->E) {
+            if ((e = hipMalloc(&q->d_keys, (size_t)max_batch * q->E * sizeof(uint32_t))) != hipSuccess)
+                return cleanup((fail("hipMalloc(keys)", e), -ENOMEM));
+        }
+    }
+    *out = q;
+    return 0;
+}
+
+int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
+{
+    if (!q)
+        return -EINVAL;
+    (void)hipSetDevice(q->device);
+    if (q->stream)
+        (void)hipStreamSynchronize(q->stream);
+    for (auto& r : q->regs)
+        (void)hipHostUnregister(r.host);
+    for (auto& p : q->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto ev : q->ev_free)
+        (void)hipEventDestroy(ev);
+    (void)hipFree(q->d_hist);
+    (void)hipFree(q->d_cum);
+    (void)hipFree(q->d_batch);
+    (void)hipFree(q->d_keys);
+    (void)hipFree(q->d_desc);
+    (void)hipFree(q->d_res);
+    if (q->own_stream)
+        (void)hipStreamDestroy(q->own_stream);
+    delete q;
+    return 0;
+}
+
+int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* s)
+{
+    if (!q)
+        return -EINVAL;
+    q->stream = s ? (hipStream_t)s : q->own_stream;
+    return 0;
+}
+
+void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q) { return q ? (void*)q->stream : nullptr; }
+
+int dqdk_gpu_rx_batch_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
+                             const dqdk_gpu_desc_t* d_desc, uint32_t n, dqdk_gpu_rx_result_t* d_results,
+                             uint32_t* d_keys)
+{
+    if (!q || !d_umem || !d_desc || !d_results)
+        return fail_errno(-EINVAL, "rx_batch_device: null argument");
+    if (n > q->max_batch)
+        return fail_errno(-EINVAL, "rx_batch_device: n > max_batch");
+    if (umem_size % 16)
+        return fail_errno(-EINVAL, "rx_batch_device: umem_size must be a multiple of 16");
+    if (n == 0)
+        return 0;
+    HIPCHK(hipSetDevice(q->device));
+    return launch_batch(q, d_umem, umem_size, d_desc, n, d_results, d_keys);
+}
+
+int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q)
+{
+    if (!q)
+        return -EINVAL;
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    return 0;
+}
+
+int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size)
+{
+    if (!q || !umem || !size)
+        return -EINVAL;
+    HIPCHK(hipSetDevice(q->device));
+    for (auto& r : q->regs)
+        if (r.host == umem)
+            return 0;
+    HIPCHK(hipHostRegister(umem, size, hipHostRegisterMapped));
+    void* dev = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dev, umem, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(umem);
+        return fail("hipHostGetDevicePointer", e);
+    }
+    q->regs.push_back({umem, size, dev});
+    return 0;
+}
+
+int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem)
+{
+    if (!q)
+        return -EINVAL;
+    for (size_t k = 0; k < q->regs.size(); k++) {
+        if (q->regs[k].host == umem) {
+            HIPCHK(hipSetDevice(q->device));
+            HIPCHK(hipStreamSynchronize(q->stream));
+            HIPCHK(hipHostUnregister(umem));
+            q->regs.erase(q->regs.begin() + (long)k);
+            return 0;
+        }
+    }
+    return -ENOENT;
+}
+
+int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,
+                      uint32_t n, dqdk_gpu_rx_result_t* per_pkt, dqdk_gpu_counters_t* delta)
+{
+    if (!q || !umem || !d || !per_pkt)
+        return fail_errno(-EINVAL, "rx_batch: null argument");
+    if (n > q->max_batch)
+        return fail_errno(-EINVAL, "rx_batch: n > max_batch");
+    if (umem_size % 16)
+        return fail_errno(-EINVAL, "rx_batch: umem_size must be a multiple of 16");
+    if (n == 0) {
+        if (delta)
+            memset(delta, 0, sizeof(*delta));
+        return 0;
+    }
+    HIPCHK(hipSetDevice(q->device));
+    const Reg* reg = nullptr;
+    for (auto& r : q->regs)
+        if ((const uint8_t*)r.host <= umem && umem + umem_size <= (const uint8_t*)r.host + r.size)
+            reg = &r;
+    if (!reg) {  // the worker registers its UMEM once (src/dqdk-mem.c:12-28 mmap+mlock)
+        int rc = dqdk_gpu_umem_register(q, (void*)umem, umem_size);
+        if (rc)
+            return rc;
+        reg = &q->regs.back();
+    }
+    const uint8_t* dev_umem = (const uint8_t*)reg->dev + (umem - (const uint8_t*)reg->host);
+    HIPCHK(hipMemcpyAsync(q->d_desc, d, (size_t)n * sizeof(*d), hipMemcpyHostToDevice, q->stream));
+    int rc = launch_batch(q, dev_umem, umem_size, q->d_desc, n, q->d_res, nullptr);
+    if (rc)
+        return rc;
+    HIPCHK(hipMemcpyAsync(per_pkt, q->d_res, (size_t)n * sizeof(*per_pkt), hipMemcpyDeviceToHost, q->stream));
+    uint64_t b[kBatchScratch];
+    HIPCHK(hipMemcpyAsync(b, q->d_batch, sizeof(b), hipMemcpyDeviceToHost, q->stream));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    if (delta)
+        memcpy(delta, &b[1], sizeof(*delta));
+    return 0;
+}
+
+int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out)
+{
+    if (!q || !out)
+        return -EINVAL;
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipMemcpyAsync(out, q->d_cum, sizeof(*out), hipMemcpyDeviceToHost, q->stream));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    return 0;
+}
+
+int dqdk_gpu_counters_reset(dqdk_gpu_queue_t* q)
+{
+    if (!q)
+        return -EINVAL;
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipMemsetAsync(q->d_cum, 0, sizeof(dqdk_gpu_counters_t), q->stream));
+    return 0;
+}
+
+int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist)
+{
+    if (!q || !host_hist)
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_get: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    HIPCHK(hipMemcpy(host_hist, q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist)
+{
+    if (!q || !host_hist)
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_accumulate: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    const size_t chunk = 64u << 20;  // entries per staging copy
+    std::vector<uint32_t> stage(chunk);
+    for (uint64_t o = 0; o < DQDK_TRISTAN_HISTO_ENTRIES; o += chunk) {
+        const size_t m = (size_t)std::min<uint64_t>(chunk, DQDK_TRISTAN_HISTO_ENTRIES - o);
+        HIPCHK(hipMemcpy(stage.data(), q->d_hist + o, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < m; k++)
+            host_hist[o + k] += stage[k];  // u32 wrap, like the shared atomic table
+    }
+    return 0;
+}
+
+int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q)
+{
+    if (!q)
+        return -EINVAL;
+    if (!q->d_hist)
+        return 0;
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipMemsetAsync(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->stream));
+    return 0;
+}
+
+uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q) { return q ? q->d_hist : nullptr; }
+
+int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on)
+{
+    if (!q)
+        return -EINVAL;
+    q->timing = on ? 1 : 0;
+    return 0;
+}
+
+int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages)
+{
+    if (!q)
+        return -EINVAL;
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    for (auto& p : q->pending) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        q->stage_ms[p.stage] += ms;
+        q->counts[p.stage] += 1;
+        q->ev_free.push_back(p.a);
+        q->ev_free.push_back(p.b);
+    }
+    q->pending.clear();
+    for (int k = 0; k < nstages && k < kStages; k++) {
+        if (stage_ms)
+            stage_ms[k] = q->stage_ms[k];
+        if (counts)
+            counts[k] = q->counts[k];
+        q->stage_ms[k] = 0;
+        q->counts[k] = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

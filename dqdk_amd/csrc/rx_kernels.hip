@@ -1,0 +1,508 @@
+/*
+ * rx_kernels.hip -- gfx950 kernels of the DQDK receive hot path.
+ * See rx_kernels.h for the kernel map and DESIGN.md for the data layout and
+ * the roofline each kernel is measured against.
+ */
+#include "rx_kernels.h"
+
+namespace dqdk {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Byte layout constants (src/tristan.h:55-60).
+constexpr uint32_t kChannels = DQDK_TRISTAN_CHANNELS;
+constexpr uint32_t kHists = DQDK_TRISTAN_HISTS;
+
+// Per-frame hand-off from phase A (lane per frame) to phase B (wave per frame).
+struct FrameInfo {
+    uint64_t addr;
+    uint64_t pseudo;   // saddr + daddr + ((17 + len16) << 8), csum_tcpudp_nofold terms
+    uint32_t datalen;
+    uint16_t len16;    // (u16)udplen handed to udp_audit_checksum
+    uint16_t check;    // udp->check as stored (LE u16)
+    uint8_t status;
+    uint8_t poff;      // payload offset from the frame start
+    uint8_t work;      // bit0 decode, bit1 udp checksum pending
+    uint8_t hs;        // ihl * 4
+};
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int b) { return (w >> (8 * b)) & 0xffu; }
+
+__device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t q)
+{
+    uint32_t lo = (q & 1) ? b : a;
+    uint32_t hi = (q & 1) ? d : c;
+    return (q & 2) ? hi : lo;
+}
+
+// bytes at rel. offset [lo, hi) of a dword starting at rel. offset p -> mask
+__device__ __forceinline__ uint32_t range_mask(int p, int lo, int hi)
+{
+    int a = lo - p, b = hi - p;
+    uint32_t ml = a <= 0 ? 0xffffffffu : (a >= 4 ? 0u : (0xffffffffu << (8 * a)));
+    uint32_t mh = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : (0xffffffffu >> (32 - 8 * b)));
+    return ml & mh;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Phase A: one lane parses one frame's headers from 112 B staged in VGPRs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameInfo& fi, dqdk_gpu_rx_result_t& r,
+                                            bool& needB)
+{
+    dqdk_gpu_desc_t d = a.desc[i];
+    const uint64_t addr = d.addr;
+    const uint32_t len = d.len;
+    const uint64_t a0 = addr & ~15ull;
+    const uint32_t off0 = (uint32_t)(addr & 15);
+
+    // 7 aligned chunks = 112 B from a0: covers frame bytes [0, 97) for any off0.
+    uint32_t w[28];
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        uint64_t o = a0 + 16ull * k;
+        if (addr < a.umem_size && o + 16 <= a.umem_size)
+            v = *(const u32x4*)(a.umem + o);
+        w[4 * k + 0] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+    // h[m] = frame dword m (frame-relative, unaligned-safe): static indices below.
+    const uint32_t q = off0 >> 2, rb = off0 & 3;
+    uint32_t s[22], h[21];
+#pragma unroll
+    for (int m = 0; m < 22; m++)
+        s[m] = sel4(w[m], w[m + 1], w[m + 2], w[m + 3], q);
+#pragma unroll
+    for (int m = 0; m < 21; m++)
+        h[m] = __builtin_amdgcn_alignbyte(s[m + 1], s[m], rb);
+
+#define FB(k) byte_of(h[(k) >> 2], (k) & 3)
+    r.datalen = 0;
+    r.status = DQDK_RX_OK;
+    r.payload_off = 0;
+    r.oob_events = 0;
+    fi.addr = addr;
+    fi.pseudo = 0;
+    fi.datalen = 0;
+    fi.len16 = 0;
+    fi.check = 0;
+    fi.poff = 0;
+    fi.work = 0;
+    fi.hs = 0;
+    needB = false;
+
+    if (a.flags & DQDK_GPU_F_PREFILTER) {  // src/bpf/forwarder.bpf.c:38-96
+        uint32_t verdict = 2;
+        uint32_t sport = (FB(34) << 8) | FB(35);
+        if (len <= 14)
+            verdict = 0;
+        else if (!(FB(12) == 0x08 && FB(13) == 0x00))
+            verdict = 1;
+        else if (len <= 34)
+            verdict = 0;
+        else if (FB(23) != 17)
+            verdict = 1;
+        else if (len <= 42)
+            verdict = 0;
+        else if (!(sport <= a.port_end && sport >= a.port_start))
+            verdict = 1;
+        if (verdict != 2) {
+            r.status = verdict == 0 ? DQDK_RX_FILTER_DROP : DQDK_RX_FILTER_PASS;
+            fi.status = r.status;
+            return;
+        }
+    }
+
+    // get_udp_payload, src/dqdk.c:185-207
+    const uint32_t tot_len = (FB(16) << 8) | FB(17);
+    const uint32_t ihl = FB(14) & 0xf;
+    const uint32_t hs = ihl * 4;
+    fi.hs = (uint8_t)hs;
+    const bool ip_ok = tot_len == ((len - 14) & 0xffffu);  // ip4_audit (u16)(len-14)
+    if (!ip_ok) {
+        r.status = DQDK_RX_INVALID_IP;
+        fi.status = r.status;
+        return;
+    }
+    if (a.flags & DQDK_GPU_F_CSUM) {
+        // ip4_audit_checksum: ~inet_csum(copy with check = 0, ihl*4) on a
+        // 4-aligned buffer -- the carry loop of inet_csum.c:92-106.
+        uint32_t res = 0, carry = 0;
+#pragma unroll
+        for (int k = 0; k < 15; k++) {
+            uint32_t wk = (h[3 + k] >> 16) | (h[4 + k] << 16);  // IP bytes 4k..4k+3
+            if (k == 2)
+                wk &= 0x0000ffffu;                           // check field zeroed
+            if ((uint32_t)k < ihl) {
+                res += carry;
+                res += wk;
+                carry = wk > res;
+            }
+        }
+        if (ihl >= 1) {
+            res += carry;
+            res = (res & 0xffff) + (res >> 16);
+        }
+        res = (res & 0xffff) + (res >> 16);  // from32to16
+        res = (res & 0xffff) + (res >> 16);
+        const uint32_t calc = (~res) & 0xffffu;
+        const uint32_t stored = FB(24) | (FB(25) << 8);
+        if (calc != stored) {
+            r.status = DQDK_RX_INVALID_IP_CSUM;
+            fi.status = r.status;
+            return;
+        }
+    }
+    const uint32_t udplen = tot_len - hs;  // u32, may wrap (dqdk.c:197)
+    // UDP header at frame byte 14 + hs: dwords 3+ihl.. with a 2-byte shift.
+    uint32_t hu1 = 0, hu2 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        if ((uint32_t)k == ihl) {
+            hu1 = h[4 + k];
+            hu2 = h[5 + k];
+        }
+    }
+    const uint32_t u47 = (hu1 >> 16) | (hu2 << 16);  // udp bytes 4..7
+    const uint32_t ulen = ((u47 & 0xff) << 8) | ((u47 >> 8) & 0xff);
+    const uint32_t ucheck = u47 >> 16;
+    if (ulen != (udplen & 0xffffu)) {  // udp_audit
+        r.status = DQDK_RX_INVALID_UDP;
+        fi.status = r.status;
+        return;
+    }
+    const uint32_t datalen = udplen - 8;  // dqdk.c:205
+    r.datalen = datalen;
+    r.payload_off = (uint8_t)(14 + hs + 8);
+    r.status = datalen ? DQDK_RX_OK : DQDK_RX_EMPTY;
+    fi.status = r.status;
+    fi.datalen = datalen;
+    fi.poff = r.payload_off;
+    const bool pending = (a.flags & DQDK_GPU_F_CSUM) && ucheck != 0;  // udp.c:12-14
+    if (pending) {
+        const uint32_t saddr = (h[6] >> 16) | (h[7] << 16);
+        const uint32_t daddr = (h[7] >> 16) | (h[8] << 16);
+        const uint32_t len16 = udplen & 0xffffu;
+        fi.len16 = (uint16_t)len16;
+        fi.check = (uint16_t)ucheck;
+        fi.pseudo = (uint64_t)saddr + (uint64_t)daddr + (uint64_t)(uint32_t)((17u + len16) << 8);
+        fi.work |= 2;
+    }
+    if (datalen != 0 && a.E != 0)
+        fi.work |= 1;
+    needB = fi.work != 0;
+#undef FB
+}
+
+// ---------------------------------------------------------------------------
+// Phase B: one wave streams one frame.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& fi_lds, uint32_t i, int lane)
+{
+    const uint64_t addr = __builtin_amdgcn_readfirstlane((uint32_t)fi_lds.addr) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fi_lds.addr >> 32)) << 32);
+    const uint32_t work = __builtin_amdgcn_readfirstlane(fi_lds.work);
+    const uint32_t poff = __builtin_amdgcn_readfirstlane(fi_lds.poff);
+    const uint32_t hs = __builtin_amdgcn_readfirstlane(fi_lds.hs);
+    const uint32_t len16 = __builtin_amdgcn_readfirstlane(fi_lds.len16);
+    const uint32_t E = a.E;
+
+    const uint64_t a0 = addr & ~15ull;
+    const int off0 = (int)(addr & 15);
+    const bool dec = work & 1, cs = work & 2;
+
+    const int dec_lo = off0 + (int)poff;
+    const int dec_hi = dec_lo + (int)(16 * E);
+    const int cs_lo = off0 + 14 + (int)hs;
+    const int cs_hi = cs_lo + (int)len16 + (int)(len16 & 1);
+    int lo = 0x7fffffff, hi = 0;
+    if (dec) {
+        lo = dec_lo;
+        hi = dec_hi;
+    }
+    if (cs) {
+        lo = min(lo, cs_lo);
+        hi = max(hi, cs_hi);
+    }
+    const int c_begin = lo >> 4, c_end = (hi + 15) >> 4;
+    const int ce0 = dec_lo >> 4;  // chunk holding event 0
+    const int sft = dec_lo & 15;  // event start within its chunk (uniform)
+    const int qd = (sft + 2) >> 2, rb = (sft + 2) & 3;
+    const bool need_next = sft >= 8;  // bytes sft+2..sft+8 cross into the next chunk
+
+    uint64_t remain = a.umem_size > a0 ? a.umem_size - a0 : 0;
+    const int nrec = (int)(remain > 0xffffffffull ? 0xffffffffull : remain);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + a0), (short)0, nrec, 0x00020000);
+
+    uint32_t acc_e = 0, acc_o = 0, oob = 0;
+    uint32_t* keys = a.keys + (uint64_t)i * E;
+
+    for (int cb = c_begin; cb < c_end; cb += 64 * kUnroll) {
+        u32x4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int c = cb + 64 * u + lane;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (c < c_end)
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, c * 16, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int c = cb + 64 * u + lane;
+            if (cb + 64 * u >= c_end)
+                break;
+            if (cs) {
+                const int p = c * 16;
+                uint32_t te = 0, to = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t wk = (k == 0 ? v[u].x : k == 1 ? v[u].y : k == 2 ? v[u].z : v[u].w) &
+                                        range_mask(p + 4 * k, cs_lo, cs_hi);
+                    te += wk & 0x00ff00ffu;
+                    to += (wk >> 8) & 0x00ff00ffu;
+                }
+                acc_e += (te & 0xffff) + (te >> 16);
+                acc_o += (to & 0xffff) + (to >> 16);
+            }
+            if (dec) {
+                const int e = c - ce0;
+                const bool has_evt = e >= 0 && e < (int)E && c < c_end;
+                uint32_t n0 = 0, n1 = 0;
+                if (need_next) {
+                    n0 = __shfl_down(v[u].x, 1);
+                    n1 = __shfl_down(v[u].y, 1);
+                    if (lane == 63 && has_evt) {
+                        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (c + 1) * 16, 0, 0);
+                        n0 = t.x;
+                        n1 = t.y;
+                    }
+                }
+                const uint32_t W0 = v[u].x, W1 = v[u].y, W2 = v[u].z, W3 = v[u].w;
+                const uint32_t w0 = qd == 0 ? W0 : qd == 1 ? W1 : qd == 2 ? W2 : qd == 3 ? W3 : n0;
+                const uint32_t w1 = qd == 0 ? W1 : qd == 1 ? W2 : qd == 2 ? W3 : qd == 3 ? n0 : n1;
+                const uint32_t w2 = qd == 0 ? W2 : qd == 1 ? W3 : qd == 2 ? n0 : qd == 3 ? n1 : 0u;
+                const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, rb);  // event bytes 2..5
+                const uint32_t y = __builtin_amdgcn_alignbyte(w2, w1, rb);  // event bytes 6..9
+                const uint32_t ch = x & 0xffffu;
+                const uint32_t bin = (x >> 24) | ((y & 0xffu) << 8);
+                const uint32_t hc = (y >> 16) & 7u;
+                const bool bad = ch >= kChannels || hc >= kHists;
+                const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
+                if (has_evt && a.keys)
+                    keys[e] = key;
+                oob += __popcll(__ballot(has_evt && bad));
+            }
+        }
+    }
+
+    if (lane == 0 || cs) {
+        uint32_t status = __builtin_amdgcn_readfirstlane(fi_lds.status);
+        if (cs) {
+            // udp_csum over [udp, udp + len16 (+1 odd)) with check zeroed:
+            // S = sum of LE u16 words relative to the udp start.
+            const uint32_t se = wave_sum(acc_e), so = wave_sum(acc_o);
+            const bool even = ((addr + 14 + hs) & 1) == 0;
+            uint32_t S = even ? se + 256u * so : so + 256u * se;
+            const uint32_t check = __builtin_amdgcn_readfirstlane(fi_lds.check);
+            if (len16 >= 7)
+                S -= check;  // udp->check = 0 before summing (udp.c:17)
+            const uint64_t pseudo = fi_lds.pseudo;
+            uint64_t t = (uint64_t)S + pseudo;           // csum_tcpudp_nofold
+            t = (t & 0xffffffffull) + (t >> 32);          // from64to32
+            t = (t & 0xffffffffull) + (t >> 32);
+            uint32_t f = (uint32_t)t;
+            f = (f & 0xffff) + (f >> 16);                 // csum_fold
+            f = (f & 0xffff) + (f >> 16);
+            const uint32_t calc = (~f) & 0xffffu;
+            if (calc != check)
+                status = DQDK_RX_INVALID_UDP_CSUM;
+            if (lane == 0 && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {
+                uint8_t* ck = const_cast<uint8_t*>(a.umem) + addr + 14 + hs + 6;
+                if (addr + 14 + hs + 8 <= a.umem_size) {
+                    ck[0] = 0;
+                    ck[1] = 0;
+                }
+            }
+        }
+        if (lane == 0) {
+            dqdk_gpu_rx_result_t r;
+            r.status = (uint8_t)status;
+            const bool ok_or_empty = status == DQDK_RX_OK || status == DQDK_RX_EMPTY;
+            r.datalen = ok_or_empty ? fi_lds.datalen : 0u;
+            r.payload_off = ok_or_empty ? (uint8_t)poff : (uint8_t)0;
+            r.oob_events = (uint16_t)(status == DQDK_RX_OK ? min(oob, 0xffffu) : 0u);
+            a.res[i] = r;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
+{
+    __shared__ FrameInfo info[kTile];
+    __shared__ int work_list[kTile];
+    __shared__ int work_count;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+
+    if (blockIdx.x == 0 && tid < 17)
+        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
+
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (tid == 0)
+            work_count = 0;
+        __syncthreads();
+        const uint32_t i = t * kTile + tid;
+        if (i < a.n) {
+            FrameInfo fi;
+            dqdk_gpu_rx_result_t r;
+            bool needB;
+            parse_frame(a, i, fi, r, needB);
+            info[tid] = fi;
+            if (needB)
+                work_list[atomicAdd(&work_count, 1)] = tid;
+            else
+                a.res[i] = r;
+        }
+        __syncthreads();
+        const int nw = work_count;
+        for (int j = wave; j < nw; j += kWaves) {
+            const int slot = work_list[j];
+            stream_frame(a, info[slot], t * kTile + slot, lane);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Counters (fetch_xsk accounting, src/dqdk.c:252-322; tristan.c:327-328).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool in_batch(uint32_t st)
+{
+    return st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
+}
+
+__global__ void __launch_bounds__(256) rx_abort_kernel(CountArgs a)
+{
+    uint64_t m = a.n;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
+        const uint32_t st = a.res[i].status;
+        if (in_batch(st) && st != DQDK_RX_OK) {
+            m = i;
+            break;  // grid-stride order: later i of this thread are larger
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t x = __shfl_xor(m, o);
+        m = x < m ? x : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m < a.n)
+        atomicMin((unsigned long long*)&a.batch_scratch[0], (unsigned long long)m);
+}
+
+enum { C_FRAMES, C_PKTS, C_BYTES, C_IP, C_UDP, C_EVENTS, C_TBYTES, C_OOB, C_EMPTY, C_FILT, C_N };
+
+__global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
+{
+    __shared__ uint64_t red[C_N][4];
+    const uint64_t abort_idx = a.batch_scratch[0];
+    const uint64_t limit = (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (abort_idx < a.n ? abort_idx + 1 : a.n) : a.n;
+    uint64_t c[C_N];
+#pragma unroll
+    for (int k = 0; k < C_N; k++)
+        c[k] = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
+        const dqdk_gpu_rx_result_t r = a.res[i];
+        const uint32_t st = r.status;
+        if (!in_batch(st)) {
+            c[C_FILT]++;
+            continue;
+        }
+        c[C_FRAMES]++;
+        if (i >= limit)
+            continue;
+        c[C_PKTS]++;
+        c[C_IP] += (st == DQDK_RX_INVALID_IP || st == DQDK_RX_INVALID_IP_CSUM);
+        c[C_UDP] += (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM);
+        c[C_EMPTY] += (st == DQDK_RX_EMPTY);
+        if (st == DQDK_RX_OK) {
+            c[C_BYTES] += r.datalen;
+            c[C_TBYTES] += r.datalen;
+            c[C_EVENTS] += a.E;
+            c[C_OOB] += a.histo ? r.oob_events : 0u;
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < C_N; k++) {
+        uint64_t v = c[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v += __shfl_xor(v, o);
+        if (lane == 0)
+            red[k][wave] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < C_N) {
+        const int k = threadIdx.x;
+        const uint64_t v = red[k][0] + red[k][1] + red[k][2] + red[k][3];
+        if (v) {
+            unsigned long long* b = (unsigned long long*)&a.batch_scratch[1];
+            unsigned long long* cum = (unsigned long long*)a.cum;
+            const int slot = k < C_EVENTS ? k : k + 1;  // dqdk_gpu_counters_t order (skip failing_batches)
+            atomicAdd(&b[slot], (unsigned long long)v);
+            atomicAdd(&cum[slot], (unsigned long long)v);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        unsigned long long* b = (unsigned long long*)&a.batch_scratch[1];
+        unsigned long long* cum = (unsigned long long*)a.cum;
+        const unsigned long long failed = abort_idx < a.n ? 1ull : 0ull;
+        if (failed) {
+            atomicAdd(&b[5], failed);    // failing_batches
+            atomicAdd(&cum[5], failed);
+        }
+        b[11] = abort_idx;               // first_abort_idx of this batch
+        cum[11] = abort_idx;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Histogram accumulation: one wave per frame, relaxed agent-scope atomics.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rx_histo_kernel(HistoArgs a)
+{
+    const uint64_t abort_idx = a.batch_scratch[0];
+    const uint32_t limit =
+        (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (uint32_t)(abort_idx < a.n ? abort_idx : a.n) : a.n;
+    const int lane = threadIdx.x & 63;
+    const uint32_t gw = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint32_t nw = (gridDim.x * 256) >> 6;
+    for (uint32_t i = gw; i < limit; i += nw) {
+        if (a.res[i].status != DQDK_RX_OK)
+            continue;
+        const uint32_t* k = a.keys + (uint64_t)i * a.E;
+        for (uint32_t e = lane; e < a.E; e += 64) {
+            const uint32_t key = k[e];
+            if (key != DQDK_KEY_NONE)
+                __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace dqdk

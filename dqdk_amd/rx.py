@@ -1,0 +1,190 @@
+"""Host-side mirror of DQDK's receive-path plugin interface over the GPU engine.
+
+Reference interface being mirrored (src/dqdk.h, src/tristan.c):
+
+* ``dqdk_ctx_init(..., payloadsz, ..., proc, ...)`` + ``tristan_init`` pick the
+  mode and the frame processor -> :class:`RxQueue` (one per RX queue / GPU).
+* ``fetch_xsk`` (src/dqdk.c:252-322) hands a peeked batch of ``xdp_desc`` to
+  ``process_frame`` one by one -> :meth:`RxQueue.process_batch` hands the whole
+  batch to ``dqdk_gpu_rx_batch`` (host UMEM) and :meth:`RxQueue.process_device`
+  to ``dqdk_gpu_rx_batch_device`` (device-resident UMEM).
+* ``dqdk_stats_t`` / ``tristan_t`` counters -> :meth:`RxQueue.counters`.
+* ``tristan_t::histo`` -> :meth:`RxQueue.histogram`.
+
+Return conventions follow the reference: failures raise :class:`DqdkError`
+carrying the negative errno the C ABI returned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+def events_per_payload(mode: int, payloadsz: int) -> int:
+    """get_energy_events_count, src/tristan.c:72-85."""
+    if mode in (L.MODE_LISTMODE, L.MODE_ENERGYHISTO):
+        return payloadsz // 16
+    if mode in (L.MODE_LISTWAVE, L.MODE_WAVEFORM):
+        return 1
+    return 0
+
+
+def histo_enabled(mode: int, flags: int) -> bool:
+    """is_store_histo, src/tristan.c:65-70."""
+    return not (flags & L.F_NO_HISTO) and mode in (L.MODE_LISTWAVE, L.MODE_LISTMODE, L.MODE_ENERGYHISTO)
+
+
+@dataclass
+class RxConfig:
+    payloadsz: int = 3392                 # -s default (src/tristan.c:419)
+    mode: int = L.MODE_ENERGYHISTO
+    flags: int = 0
+    port_start: int = 0
+    port_end: int = 0
+
+    def to_c(self) -> L.Cfg:
+        return L.Cfg(self.payloadsz, self.mode, self.flags, self.port_start, self.port_end)
+
+    @property
+    def events(self) -> int:
+        return events_per_payload(self.mode, self.payloadsz)
+
+
+def device_count() -> int:
+    return L.lib().dqdk_gpu_device_count()
+
+
+class RxQueue:
+    """One RX queue bound to one GPU (the reference's dqdk_worker_t)."""
+
+    def __init__(self, device: int, cfg: RxConfig, max_batch: int):
+        self.cfg = cfg
+        self.device = device
+        self.max_batch = max_batch
+        h = C.c_void_p()
+        L.check(L.lib().dqdk_gpu_queue_create(device, C.byref(cfg.to_c()), max_batch, C.byref(h)),
+                "dqdk_gpu_queue_create")
+        self._h = h
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            L.lib().dqdk_gpu_queue_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream_ptr: int | None) -> None:
+        L.check(L.lib().dqdk_gpu_queue_set_stream(self._h, hip_stream_ptr or None), "set_stream")
+
+    def sync(self) -> None:
+        L.check(L.lib().dqdk_gpu_queue_sync(self._h), "queue_sync")
+
+    # -- batches -----------------------------------------------------------
+    def process_device(self, umem_ptr: int, umem_size: int, desc_ptr: int, n: int,
+                       results_ptr: int, keys_ptr: int | None = None) -> None:
+        """Async device-resident batch: all pointers are device pointers."""
+        L.check(L.lib().dqdk_gpu_rx_batch_device(self._h, umem_ptr, umem_size, desc_ptr, n,
+                                                 results_ptr, keys_ptr or None),
+                "dqdk_gpu_rx_batch_device")
+
+    def process_batch(self, umem: np.ndarray, desc: np.ndarray) -> tuple[np.ndarray, dict]:
+        """Host drop-in for the loop at src/dqdk.c:291-298 (synchronous).
+
+        ``umem`` is the host UMEM (uint8, registered/pinned on first use),
+        ``desc`` a DESC_DTYPE array.  Returns (per-frame results, counter delta).
+        """
+        assert umem.dtype == np.uint8 and umem.flags.c_contiguous
+        desc = np.ascontiguousarray(desc, dtype=L.DESC_DTYPE)
+        n = len(desc)
+        res = np.zeros(n, dtype=L.RESULT_DTYPE)
+        delta = L.Counters()
+        L.check(L.lib().dqdk_gpu_rx_batch(self._h, umem.ctypes.data, umem.nbytes, desc.ctypes.data, n,
+                                          res.ctypes.data, C.byref(delta)), "dqdk_gpu_rx_batch")
+        return res, delta.as_dict()
+
+    def register_umem(self, umem: np.ndarray) -> None:
+        L.check(L.lib().dqdk_gpu_umem_register(self._h, umem.ctypes.data, umem.nbytes), "umem_register")
+
+    def unregister_umem(self, umem: np.ndarray) -> None:
+        L.check(L.lib().dqdk_gpu_umem_unregister(self._h, umem.ctypes.data), "umem_unregister")
+
+    # -- egress ------------------------------------------------------------
+    def counters(self) -> dict:
+        c = L.Counters()
+        L.check(L.lib().dqdk_gpu_counters_get(self._h, C.byref(c)), "counters_get")
+        return c.as_dict()
+
+    def reset_counters(self) -> None:
+        L.check(L.lib().dqdk_gpu_counters_reset(self._h), "counters_reset")
+
+    def histogram(self, out: np.ndarray | None = None) -> np.ndarray:
+        """The queue's u32[1512*6*65536] histogram (src/tristan.h:71-77)."""
+        if out is None:
+            out = np.empty(L.HISTO_ENTRIES, dtype=np.uint32)
+        assert out.dtype == np.uint32 and out.size == L.HISTO_ENTRIES and out.flags.c_contiguous
+        L.check(L.lib().dqdk_gpu_histogram_get(self._h, out.ctypes.data), "histogram_get")
+        return out
+
+    def accumulate_histogram(self, into: np.ndarray) -> None:
+        assert into.dtype == np.uint32 and into.size == L.HISTO_ENTRIES and into.flags.c_contiguous
+        L.check(L.lib().dqdk_gpu_histogram_accumulate(self._h, into.ctypes.data), "histogram_accumulate")
+
+    def reset_histogram(self) -> None:
+        L.check(L.lib().dqdk_gpu_histogram_reset(self._h), "histogram_reset")
+
+    def histogram_device_ptr(self) -> int | None:
+        return L.lib().dqdk_gpu_histogram_device_ptr(self._h)
+
+    # -- stage timing --------------------------------------------------------
+    def enable_timing(self, on: bool = True) -> None:
+        L.check(L.lib().dqdk_gpu_timing_enable(self._h, int(on)), "timing_enable")
+
+    def read_timing(self) -> dict:
+        ms = (C.c_double * 3)()
+        cnt = (C.c_uint64 * 3)()
+        L.check(L.lib().dqdk_gpu_timing_read(self._h, ms, cnt, 3), "timing_read")
+        names = ("rx_decode", "counters", "histogram")
+        return {names[k]: {"ms": ms[k], "launches": int(cnt[k])} for k in range(3)}
+
+
+# ---- synthetic UMEM (bench / test input) ------------------------------------
+
+SEED = 20261015
+
+
+def synth_cfg(frame_len: int, stride: int, queue: int = 0, faulty: bool = False, seed: int = SEED) -> L.SynthCfg:
+    return L.SynthCfg(seed, queue, frame_len, stride, int(faulty))
+
+
+def synth_umem(n: int, frame_len: int, stride: int, queue: int = 0, faulty: bool = False, seed: int = SEED,
+               first: int = 0, threads: int = 8, pad: int = 0, out: np.ndarray | None = None
+               ) -> tuple[np.ndarray, np.ndarray]:
+    """Fill a host UMEM image with n synthetic frames; returns (umem u8, desc)."""
+    c = synth_cfg(frame_len, stride, queue, faulty, seed)
+    size = int(L.lib().dqdk_synth_umem_size(C.byref(c), n)) + pad
+    size = (size + 15) // 16 * 16
+    umem = out if out is not None else np.empty(size, dtype=np.uint8)
+    assert umem.nbytes >= size
+    desc = np.zeros(n, dtype=L.DESC_DTYPE)
+    L.check(L.lib().dqdk_synth_frames(C.byref(c), first, n, umem.ctypes.data, umem.nbytes, desc.ctypes.data,
+                                      threads), "dqdk_synth_frames")
+    return umem, desc

@@ -1,0 +1,191 @@
+/*
+ * dqdk_gpu.h -- C ABI of the MI355X receive-path engine (libdqdk_gpu.so).
+ *
+ * Drop-in boundary for DQDK's per-frame receive hot path.  The reference
+ * runs, per RX descriptor, on one worker pthread per queue:
+ *
+ *   fetch_xsk            src/dqdk.c:252-322   (per-descriptor loop :291-298)
+ *     process_frame      src/dqdk.c:231-250
+ *       get_udp_payload  src/dqdk.c:185-207   -> ip4_audit  src/tcpip/ipv4.c:13-20
+ *                                             -> udp_audit  src/tcpip/udp.c:22-31
+ *       frame_processor  src/dqdk.h:84-85  == process_unbuffered_frame src/tristan.c:377-381
+ *         tristan_process            src/tristan.c:308-330
+ *           process_events_unrolled16 src/tristan.c:247-304
+ *             histogram_event         src/tristan.c:233-245
+ *
+ * dqdk_gpu_rx_batch() replaces the loop at src/dqdk.c:291-298 for a whole
+ * peeked batch (the ring ops around it are unchanged) and runs
+ * get_udp_payload + the TRISTAN sync frame processor on the GPU.  The
+ * optional checksum configuration (ip4_audit_checksum src/tcpip/ipv4.c:6-11,
+ * udp_audit_checksum src/tcpip/udp.c:10-20, both commented out of the audit
+ * in the shipped code at ipv4.c:16 / udp.c:26) and the XDP forwarder's
+ * predicate (src/bpf/forwarder.bpf.c:38-96) are selectable per queue.
+ *
+ * Plain C types only; every pointer is either a host pointer or a device
+ * pointer as each function states.  Errors are negative errno values like
+ * the reference (-EINVAL, -ENOMEM, -ENODEV; HIP failures map to -EIO).
+ * There is no CPU implementation behind any of these entry points: without
+ * a usable gfx950 device, dqdk_gpu_queue_create() returns -ENODEV.
+ */
+#ifndef DQDK_GPU_H
+#define DQDK_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQDK_GPU_ABI_VERSION 1
+
+/* struct xdp_desc from linux/if_xdp.h: frame = umem + addr (src/dqdk.c:293) */
+typedef struct dqdk_gpu_desc {
+    uint64_t addr;
+    uint32_t len;
+    uint32_t options;
+} dqdk_gpu_desc_t;
+
+/* Per-frame verdict.  OK is the only status for which the reference calls
+ * the frame processor; every other in-batch status makes process_frame
+ * return -ENOBUFS (src/dqdk.c:243-249). */
+enum dqdk_gpu_status {
+    DQDK_RX_OK = 0,
+    DQDK_RX_INVALID_IP = 1,       /* ip4_audit: ntohs(tot_len) != (u16)(len-14)   */
+    DQDK_RX_INVALID_UDP = 2,      /* udp_audit: ntohs(udp->len) != (u16)udplen    */
+    DQDK_RX_EMPTY = 3,            /* valid headers but datalen == 0               */
+    DQDK_RX_INVALID_IP_CSUM = 4,  /* checksum config: ip4_audit_checksum failed   */
+    DQDK_RX_INVALID_UDP_CSUM = 5, /* checksum config: udp_audit_checksum failed   */
+    DQDK_RX_FILTER_DROP = 6,      /* prefilter: forwarder would XDP_DROP          */
+    DQDK_RX_FILTER_PASS = 7,      /* prefilter: forwarder would XDP_PASS          */
+};
+
+/* 8-B per-frame record (the `datalen` out-param + payload pointer of
+ * get_udp_payload, plus the verdict). */
+typedef struct dqdk_gpu_rx_result {
+    uint32_t datalen;     /* udplen - 8 in u32, may wrap (src/dqdk.c:205) */
+    uint8_t status;       /* enum dqdk_gpu_status                          */
+    uint8_t payload_off;  /* payload = umem + addr + payload_off (OK/EMPTY) */
+    uint16_t oob_events;  /* events histogram_event rejected (saturating)  */
+} dqdk_gpu_rx_result_t;
+
+/* Counters: the dqdk_stats_t fields this path touches (src/dqdk.h:52-68)
+ * plus the tristan_t atomics (src/tristan.h:81-82) and a few diagnostics. */
+typedef struct dqdk_gpu_counters {
+    uint64_t rcvd_frames;      /* dqdk.c:289                               */
+    uint64_t rcvd_pkts;        /* dqdk.c:189                               */
+    uint64_t rcvd_bytes;       /* dqdk.c:246                               */
+    uint64_t invalid_ip_pkts;  /* dqdk.c:192                               */
+    uint64_t invalid_udp_pkts; /* dqdk.c:201                               */
+    uint64_t failing_batches;  /* dqdk.c:319                               */
+    uint64_t total_events;     /* tristan.c:328                            */
+    uint64_t total_bytes;      /* tristan.c:327                            */
+    uint64_t oob_events;       /* tristan.c:236-240 (logged there)         */
+    uint64_t empty_pkts;       /* datalen == 0 frames                      */
+    uint64_t filtered_frames;  /* prefilter non-REDIRECT frames            */
+    uint64_t first_abort_idx;  /* last batch: first failing index, or n    */
+} dqdk_gpu_counters_t;
+
+/* tristan_mode_t (src/tristan.h:62-67) */
+enum dqdk_gpu_mode {
+    DQDK_MODE_WAVEFORM = 0,
+    DQDK_MODE_LISTWAVE = 1,
+    DQDK_MODE_LISTMODE = 2,
+    DQDK_MODE_ENERGYHISTO = 3,
+};
+
+enum dqdk_gpu_flags {
+    DQDK_GPU_F_CSUM = 1u << 0,           /* verify IPv4 + UDP checksums                 */
+    DQDK_GPU_F_BATCH_ABORT = 1u << 1,    /* account like fetch_xsk: stop at 1st failure */
+    DQDK_GPU_F_PREFILTER = 1u << 2,      /* apply the XDP forwarder predicate first     */
+    DQDK_GPU_F_NO_HISTO = 1u << 3,       /* decode only, no histogram accumulation      */
+    DQDK_GPU_F_CSUM_WRITEBACK = 1u << 4, /* zero udp->check in UMEM like udp.c:17       */
+};
+
+typedef struct dqdk_gpu_cfg {
+    uint32_t payloadsz;  /* -s (src/tristan.c:419): events per frame = payloadsz/16 */
+    uint32_t mode;       /* enum dqdk_gpu_mode                                        */
+    uint32_t flags;      /* enum dqdk_gpu_flags                                       */
+    uint16_t port_start; /* prefilter source-port range (dqdk_for_ports_range)        */
+    uint16_t port_end;
+} dqdk_gpu_cfg_t;
+
+/* Histogram geometry (src/tristan.h:55-60): u32[1512][6][65536]. */
+#define DQDK_TRISTAN_CHANNELS 1512u
+#define DQDK_TRISTAN_HISTS 6u
+#define DQDK_TRISTAN_BINS 65536u
+#define DQDK_TRISTAN_HISTO_ENTRIES ((uint64_t)DQDK_TRISTAN_CHANNELS * DQDK_TRISTAN_HISTS * DQDK_TRISTAN_BINS)
+#define DQDK_KEY_NONE 0xFFFFFFFFu /* decoded record of an out-of-bounds event */
+
+typedef struct dqdk_gpu_queue dqdk_gpu_queue_t;
+
+/* ---- lifecycle ----------------------------------------------------------- */
+int dqdk_gpu_abi_version(void);
+int dqdk_gpu_device_count(void);
+/* One queue per RX queue / worker thread (src/dqdk.c:517-620).  Allocates
+ * the queue's device histogram (2.38 GB, zeroed) unless the mode has none. */
+int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_batch, dqdk_gpu_queue_t** out);
+int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q);
+/* Run the queue's work on an existing hipStream_t (NULL = its own stream). */
+int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* hip_stream);
+void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q);
+
+/* ---- device-resident batch (async on the queue stream) ------------------- */
+/* d_umem/d_desc/d_results/d_keys are DEVICE pointers.  d_keys (nullable)
+ * receives n*E u32 decoded records: key = (channel*6 + hist_class)*65536 +
+ * (energy>>8), DQDK_KEY_NONE for out-of-bounds events; records of frames
+ * whose status is not OK are unspecified.  Counters accumulate on device. */
+int dqdk_gpu_rx_batch_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
+                             const dqdk_gpu_desc_t* d_desc, uint32_t n, dqdk_gpu_rx_result_t* d_results,
+                             uint32_t* d_keys);
+int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
+
+/* ---- host drop-in for the fetch_xsk loop (synchronous) ------------------- */
+/* umem: host UMEM (pinned once through dqdk_gpu_umem_register for best
+ * rate); d, per_pkt, delta: host pointers.  Copies the batch's frames in,
+ * runs the batch, copies per-frame results and this batch's counter delta
+ * out.  Returns 0, or the negative errno of the first failure. */
+int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size);
+int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
+int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,
+                      uint32_t n, dqdk_gpu_rx_result_t* per_pkt, dqdk_gpu_counters_t* delta);
+
+/* ---- counters / histogram egress ----------------------------------------- */
+int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out); /* cumulative */
+int dqdk_gpu_counters_reset(dqdk_gpu_queue_t* q);
+/* Copy the queue's u32[DQDK_TRISTAN_HISTO_ENTRIES] histogram to host memory. */
+int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist);
+/* Add (u32 wrap) the queue's histogram into host_hist: the end-of-run merge
+ * of per-GPU partials into the one tristan_histo_t (src/tristan.c:97). */
+int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist);
+int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
+/* Device pointer of the histogram (for RCCL reduce across GPUs), or NULL. */
+uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
+
+/* ---- stage timing (HIP events on the queue stream) ------------------------ */
+/* When enabled, every kernel of every batch is bracketed by hipEvents on the
+ * queue stream; stage_ms[k] accumulates milliseconds for stage k
+ * (0 = rx_decode, 1 = finalize, 2 = histogram), counts[k] = launches. */
+int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on);
+int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages);
+
+const char* dqdk_gpu_last_error(void);
+
+/* ---- synthetic UMEM generator (bench/test input only; host C) ------------ */
+typedef struct dqdk_synth_cfg {
+    uint64_t seed;      /* counter-based PRNG seed (20261015) */
+    uint32_t queue;     /* RX queue id: UDP source port 5000+queue           */
+    uint32_t frame_len; /* L; 0 = seeded 50/50 mix of 1500 and 9000 B        */
+    uint32_t stride;    /* UMEM bytes per frame slot (4096, 9216, ...)       */
+    uint32_t faulty;    /* inject header/checksum/event faults               */
+} dqdk_synth_cfg_t;
+
+uint64_t dqdk_synth_umem_size(const dqdk_synth_cfg_t* c, uint32_t n);
+uint32_t dqdk_synth_frame_len(const dqdk_synth_cfg_t* c, uint64_t frame_index);
+/* Fill umem[0, n*stride) with frames first..first+n-1 and their descriptors. */
+int dqdk_synth_frames(const dqdk_synth_cfg_t* c, uint64_t first, uint32_t n, uint8_t* umem, uint64_t umem_size,
+                      dqdk_gpu_desc_t* d, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
