@@ -211,8 +211,9 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& fi_lds, uint32_t i, int lane)
 {
-    const uint64_t addr = __builtin_amdgcn_readfirstlane((uint32_t)fi_lds.addr) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fi_lds.addr >> 32)) << 32);
+    // readfirstlane returns int: widen through uint32_t or the low word sign-extends
+    const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fi_lds.addr) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(fi_lds.addr >> 32)) << 32);
     const uint32_t work = __builtin_amdgcn_readfirstlane(fi_lds.work);
     const uint32_t poff = __builtin_amdgcn_readfirstlane(fi_lds.poff);
     const uint32_t hs = __builtin_amdgcn_readfirstlane(fi_lds.hs);
