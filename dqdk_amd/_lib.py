@@ -64,6 +64,7 @@ MODE_WAVEFORM, MODE_LISTWAVE, MODE_LISTMODE, MODE_ENERGYHISTO = range(4)
 MODES = {"waveform": MODE_WAVEFORM, "listwave": MODE_LISTWAVE, "listmode": MODE_LISTMODE,
          "energy-histo": MODE_ENERGYHISTO}  # src/tristan.c:13-18
 F_CSUM, F_BATCH_ABORT, F_PREFILTER, F_NO_HISTO, F_CSUM_WRITEBACK = 1, 2, 4, 8, 16
+F_HISTO_ATOMIC, F_HISTO_PARTITIONED = 32, 64
 KEY_NONE = 0xFFFFFFFF
 HISTO_CHANNELS, HISTO_HISTS, HISTO_BINS = 1512, 6, 65536
 HISTO_ENTRIES = HISTO_CHANNELS * HISTO_HISTS * HISTO_BINS

@@ -81,6 +81,10 @@ struct dqdk_gpu_queue {
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
     uint32_t* d_keys = nullptr;
+    uint32_t* d_part1 = nullptr;   // partitioned-histogram staging (max_batch * E each)
+    uint32_t* d_part2 = nullptr;
+    uint32_t* d_hscratch = nullptr;
+    int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     dqdk_gpu_desc_t* d_desc = nullptr;
     dqdk_gpu_rx_result_t* d_res = nullptr;
     std::vector<Reg> regs;
@@ -127,6 +131,18 @@ struct StageTimer {
     }
 };
 
+// The partitioned histogram sweeps every slice that receives events (up to
+// the whole 2.38 GB table once per batch); per-event atomics cost ~1/18 ns
+// each (measured, profiles/).  Partition once a batch carries enough events.
+constexpr uint64_t kPartitionMinKeys = 4u << 20;
+
+bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)
+{
+    if (q->histo_path)
+        return q->histo_path == 2;
+    return (uint64_t)n * q->E >= kPartitionMinKeys;
+}
+
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
 {
@@ -146,6 +162,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ra.port_start = q->cfg.port_start;
     ra.port_end = q->cfg.port_end;
     ra.batch_scratch = q->d_batch;
+    const bool partitioned = q->histo && q->E && use_partitioned(q, n);
+    ra.cnt1 = partitioned ? q->d_hscratch + kOffCnt1 : nullptr;
+    if (partitioned)
+        HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kHistScratchWords * sizeof(uint32_t), q->stream));
 
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t grid_dec = std::min<uint32_t>(ntiles, (uint32_t)q->cu_count * 8u);
@@ -177,12 +197,27 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.keys = keys;
         ha.n = n;
         ha.E = q->E;
+        ha.E_magic = 0xffffffffu / q->E;
         ha.flags = q->cfg.flags;
         ha.batch_scratch = q->d_batch;
         ha.hist = q->d_hist;
-        const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
+        ha.scratch = q->d_hscratch;
+        ha.part1 = q->d_part1;
+        ha.part2 = q->d_part2;
         StageTimer t(q, 2);
-        hipLaunchKernelGGL(rx_histo_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
+        if (!partitioned) {
+            const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
+            hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
+        } else {
+            const uint64_t nkeys = (uint64_t)n * q->E;
+            const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
+            const uint32_t grid_p = std::min<uint32_t>(chunks, (uint32_t)q->cu_count * 2u);
+            const uint32_t grid_l2 = std::min<uint32_t>(chunks + kL1Buckets, (uint32_t)q->cu_count * 2u);
+            hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kPartThreads), 0, q->stream, ha);
+            hipLaunchKernelGGL(rx_part2_count_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+            hipLaunchKernelGGL(rx_part2_scatter_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+            hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+        }
         HIPCHK(hipGetLastError());
     }
     return 0;
@@ -211,6 +246,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     *out = nullptr;
     if (cfg->mode > DQDK_MODE_ENERGYHISTO || cfg->payloadsz > (16u << 20))
         return fail_errno(-EINVAL, "queue_create: bad mode or payloadsz");
+    if ((uint64_t)max_batch * events_per_payload(cfg->mode, cfg->payloadsz) >= (1ull << 31))
+        return fail_errno(-EINVAL, "queue_create: max_batch * events per frame must be < 2^31");
     int ndev = dqdk_gpu_device_count();
     if (device < 0 || device >= ndev)
         return fail_errno(-ENODEV, "queue_create: no such HIP device");
@@ -229,6 +266,10 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                (cfg->mode == DQDK_MODE_LISTWAVE || cfg->mode == DQDK_MODE_LISTMODE ||
                 cfg->mode == DQDK_MODE_ENERGYHISTO);  // is_store_histo, src/tristan.c:65-70
     q->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (cfg->flags & DQDK_GPU_F_HISTO_ATOMIC)
+        q->histo_path = 1;
+    else if (cfg->flags & DQDK_GPU_F_HISTO_PARTITIONED)
+        q->histo_path = 2;
 
     auto cleanup = [&](int rc) {
         dqdk_gpu_queue_destroy(q);
@@ -252,8 +293,11 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
-            if ((e = hipMalloc(&q->d_keys, (size_t)max_batch * q->E * sizeof(uint32_t))) != hipSuccess)
-                return cleanup((fail("hipMalloc(keys)", e), -ENOMEM));
+            const size_t kb = (size_t)max_batch * q->E * sizeof(uint32_t);
+            if ((e = hipMalloc(&q->d_keys, kb)) != hipSuccess || (e = hipMalloc(&q->d_part1, kb)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part2, kb)) != hipSuccess ||
+                (e = hipMalloc(&q->d_hscratch, kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
+                return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
         }
     }
     *out = q;
@@ -279,6 +323,9 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_cum);
     (void)hipFree(q->d_batch);
     (void)hipFree(q->d_keys);
+    (void)hipFree(q->d_part1);
+    (void)hipFree(q->d_part2);
+    (void)hipFree(q->d_hscratch);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     if (q->own_stream)

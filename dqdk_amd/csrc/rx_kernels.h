@@ -12,8 +12,14 @@
  *                 src/tristan.c:233-245).
  * K2 rx_abort / rx_count : per-batch counters of fetch_xsk (src/dqdk.c:252-322)
  *                 under per-packet or batch-abort accounting.
- * K3 rx_histo   : histogram accumulation of the keys of accounted OK frames
- *                 (relaxed atomic increment, src/tristan.c:243).
+ * K3 histogram accumulation of the keys of accounted OK frames (the relaxed
+ *    atomic increment of src/tristan.c:243), two interchangeable forms:
+ *    - rx_histo_atomic: one device-scope atomic per event (small batches);
+ *    - partitioned: rx_part1 (keys -> 284 buckets of 2^21 bins),
+ *      rx_part2_count / rx_part2_scatter (bucket -> 16K-bin slices),
+ *      rx_slice_histo (LDS histogram per slice + one coalesced
+ *      read-modify-write of the slice's 64 KB of table).  Same multiset of
+ *      increments, so the table is bit-identical.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -27,6 +33,24 @@ constexpr int kTile = 256;          // frames per K1 tile = threads per block
 constexpr int kWaves = kTile / 64;  // waves per block
 constexpr int kUnroll = 4;          // 1-KiB windows in flight per wave in phase B
 
+// Partitioned histogram geometry.  Keys < 1512*6*65536 = 594,542,592 < 2^30.
+constexpr int kL1Shift = 21;                                // 2^21 bins (8 MB of table) per bucket
+constexpr int kL1Buckets = 284;                             // ceil(594542592 / 2^21)
+constexpr int kSliceBits = 14;                              // 2^14 bins (64 KB LDS) per slice
+constexpr int kSubs = 1 << (kL1Shift - kSliceBits);         // 128 slices per bucket
+constexpr int kSlices = kL1Buckets * kSubs;                 // 36352 (36288 used)
+constexpr int kPartThreads = 1024;                          // part1/part2 block size
+constexpr int kPartKeysPerThread = 16;
+constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 16384 keys staged in LDS
+constexpr int kSliceThreads = 512;
+
+// u32 scratch words used by the partitioned histogram (zeroed per batch)
+constexpr int kOffCnt1 = 0;                   // [kL1Buckets] keys per bucket (decode, upper bound)
+constexpr int kOffCur1 = 288;                 // [kL1Buckets] keys written per bucket (part1)
+constexpr int kOffCnt2 = 576;                 // [kSlices]    keys per slice (part2_count)
+constexpr int kOffCur2 = kOffCnt2 + kSlices;  // [kSlices]    append cursors (part2_scatter)
+constexpr int kHistScratchWords = kOffCur2 + kSlices;
+
 struct RxArgs {
     const uint8_t* umem;
     uint64_t umem_size;
@@ -37,7 +61,8 @@ struct RxArgs {
     uint32_t E;
     uint32_t flags;
     uint32_t port_start, port_end;
-    uint64_t* batch_scratch;  // [0] = first abort idx, [1..16] = per-batch counters
+    uint64_t* batch_scratch;  // [0] = first abort idx, [1..12] = per-batch counters
+    uint32_t* cnt1;           // bucket counts for the partitioned histogram, or null
 };
 
 struct CountArgs {
@@ -55,14 +80,22 @@ struct HistoArgs {
     const uint32_t* keys;
     uint32_t n;
     uint32_t E;
+    uint32_t E_magic;  // 0xFFFFFFFF / E (floor), for key index -> frame
     uint32_t flags;
     const uint64_t* batch_scratch;
     uint32_t* hist;
+    uint32_t* scratch;  // kHistScratchWords
+    uint32_t* part1;    // n*E
+    uint32_t* part2;    // n*E
 };
 
 __global__ void rx_decode_kernel(RxArgs a);
 __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_count_kernel(CountArgs a);
-__global__ void rx_histo_kernel(HistoArgs a);
+__global__ void rx_histo_atomic_kernel(HistoArgs a);
+__global__ void rx_part1_kernel(HistoArgs a);
+__global__ void rx_part2_count_kernel(HistoArgs a);
+__global__ void rx_part2_scatter_kernel(HistoArgs a);
+__global__ void rx_slice_histo_kernel(HistoArgs a);
 
 }  // namespace dqdk

@@ -209,7 +209,8 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
 // ---------------------------------------------------------------------------
 // Phase B: one wave streams one frame.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& fi_lds, uint32_t i, int lane)
+__device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& fi_lds, uint32_t i, int lane,
+                                             uint32_t* lds_cnt1)
 {
     // readfirstlane returns int: widen through uint32_t or the low word sign-extends
     const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fi_lds.addr) |
@@ -304,6 +305,8 @@ __device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& f
                 const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
                 if (has_evt && a.keys)
                     keys[e] = key;
+                if (a.cnt1 && has_evt && !bad)
+                    atomicAdd(&lds_cnt1[key >> kL1Shift], 1u);  // capacity of the key's L1 bucket
                 oob += __popcll(__ballot(has_evt && bad));
             }
         }
@@ -355,9 +358,14 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
     __shared__ FrameInfo info[kTile];
     __shared__ int work_list[kTile];
     __shared__ int work_count;
+    __shared__ uint32_t lds_cnt1[kL1Buckets];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
+    if (a.cnt1) {
+        for (int b = tid; b < kL1Buckets; b += kTile)
+            lds_cnt1[b] = 0;
+    }
 
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
@@ -383,9 +391,15 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
         const int nw = work_count;
         for (int j = wave; j < nw; j += kWaves) {
             const int slot = work_list[j];
-            stream_frame(a, info[slot], t * kTile + slot, lane);
+            stream_frame(a, info[slot], t * kTile + slot, lane, lds_cnt1);
         }
         __syncthreads();
+    }
+    if (a.cnt1) {
+        __syncthreads();
+        for (int b = tid; b < kL1Buckets; b += kTile)
+            if (lds_cnt1[b])
+                atomicAdd(&a.cnt1[b], lds_cnt1[b]);
     }
 }
 
@@ -484,13 +498,39 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Histogram accumulation: one wave per frame, relaxed agent-scope atomics.
+// Histogram accumulation (src/tristan.c:233-245, :243 relaxed atomic ++).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) rx_histo_kernel(HistoArgs a)
+__device__ __forceinline__ uint32_t frames_limit(const HistoArgs& a)
 {
     const uint64_t abort_idx = a.batch_scratch[0];
-    const uint32_t limit =
-        (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (uint32_t)(abort_idx < a.n ? abort_idx : a.n) : a.n;
+    return (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (uint32_t)(abort_idx < a.n ? abort_idx : a.n) : a.n;
+}
+
+// key index p -> frame p / E (E_magic = floor(0xFFFFFFFF / E), error <= 2)
+__device__ __forceinline__ uint32_t key_frame(const HistoArgs& a, uint32_t p)
+{
+    uint32_t q = __umulhi(p, a.E_magic);
+    uint32_t r = p - q * a.E;
+    while (r >= a.E) {
+        q++;
+        r -= a.E;
+    }
+    return q;
+}
+
+// the key at index p counts iff its frame is accounted and OK
+__device__ __forceinline__ bool key_counts(const HistoArgs& a, uint32_t p, uint32_t key, uint32_t limit)
+{
+    if (key == DQDK_KEY_NONE)
+        return false;
+    const uint32_t f = key_frame(a, p);
+    return f < limit && a.res[f].status == DQDK_RX_OK;
+}
+
+// Small batches: one relaxed agent-scope atomic per event, one wave per frame.
+__global__ void __launch_bounds__(256) rx_histo_atomic_kernel(HistoArgs a)
+{
+    const uint32_t limit = frames_limit(a);
     const int lane = threadIdx.x & 63;
     const uint32_t gw = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const uint32_t nw = (gridDim.x * 256) >> 6;
@@ -502,6 +542,272 @@ __global__ void __launch_bounds__(256) rx_histo_kernel(HistoArgs a)
             const uint32_t key = k[e];
             if (key != DQDK_KEY_NONE)
                 __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Exclusive scan of src[0..n) (n <= 320) into dst[0..n], dst[n] = total, by
+// wave 0 of the block (5 entries per lane).  Caller syncs afterwards.
+__device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* dst, int n, bool src_global)
+{
+    if (threadIdx.x >= 64)
+        return;
+    const int lane = threadIdx.x;
+    uint32_t v[5], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const int i = lane * 5 + j;
+        v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) : 0u;
+        sum += v[j];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o)
+            incl += t;
+    }
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const int i = lane * 5 + j;
+        if (i <= n)
+            dst[i] = run;
+        run += v[j];
+    }
+}
+
+// largest b with off[b] <= p, off[0] = 0, off monotone, b < nb
+__device__ __forceinline__ int find_run(const uint32_t* off, int nb, uint32_t p)
+{
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= p)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// Level 1: keys (frame order) -> part1, grouped by bucket = key >> 21.
+// A block stages 16K keys in LDS sorted by bucket, reserves each bucket's
+// run with one global atomic, and writes the runs out contiguously.
+__global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
+{
+    __shared__ uint32_t stage[kPartChunk];
+    __shared__ uint32_t off1[kL1Buckets + 1];
+    __shared__ uint32_t lcnt[kL1Buckets];
+    __shared__ uint32_t loff[kL1Buckets + 1];
+    __shared__ uint32_t gpos[kL1Buckets];
+    const int tid = threadIdx.x;
+    const uint32_t limit = frames_limit(a);
+    const uint32_t total = limit * a.E;
+    uint32_t* cur1 = a.scratch + kOffCur1;
+    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true);
+    for (uint32_t base = blockIdx.x * (uint32_t)kPartChunk; base < total; base += gridDim.x * (uint32_t)kPartChunk) {
+        for (int b = tid; b < kL1Buckets; b += kPartThreads)
+            lcnt[b] = 0;
+        __syncthreads();
+        uint32_t key[kPartKeysPerThread], rank[kPartKeysPerThread];
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread / 4; j++) {
+            const uint32_t p0 = base + (uint32_t)(j * kPartThreads + tid) * 4;
+            u32x4_t v = {DQDK_KEY_NONE, DQDK_KEY_NONE, DQDK_KEY_NONE, DQDK_KEY_NONE};
+            if (p0 + 3 < total) {
+                v = *(const u32x4_t*)(a.keys + p0);
+            } else {
+                if (p0 + 0 < total) v.x = a.keys[p0 + 0];
+                if (p0 + 1 < total) v.y = a.keys[p0 + 1];
+                if (p0 + 2 < total) v.z = a.keys[p0 + 2];
+            }
+            key[4 * j + 0] = v.x;
+            key[4 * j + 1] = v.y;
+            key[4 * j + 2] = v.z;
+            key[4 * j + 3] = v.w;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t k = key[4 * j + c];
+                const bool ok = p0 + c < total && key_counts(a, p0 + c, k, limit);
+                rank[4 * j + c] = ok ? atomicAdd(&lcnt[k >> kL1Shift], 1u) : 0xffffffffu;
+            }
+        }
+        __syncthreads();
+        wave0_excl_scan(lcnt, loff, kL1Buckets, false);
+        for (int b = tid; b < kL1Buckets; b += kPartThreads)
+            if (lcnt[b])
+                gpos[b] = off1[b] + atomicAdd(&cur1[b], lcnt[b]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            if (rank[j] != 0xffffffffu)
+                stage[loff[key[j] >> kL1Shift] + rank[j]] = key[j];
+        __syncthreads();
+        const uint32_t nkeys = loff[kL1Buckets];
+        for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
+            const int b = find_run(loff, kL1Buckets, p);
+            a.part1[gpos[b] + (p - loff[b])] = stage[p];
+        }
+        __syncthreads();
+    }
+}
+
+// Work items of level 2: (bucket, 16K-key chunk of the bucket's part1 run).
+struct L2Items {
+    uint32_t off1[kL1Buckets + 1];   // bucket start in part1/part2
+    uint32_t len1[kL1Buckets];       // keys written by part1
+    uint32_t istart[kL1Buckets + 1]; // first item of each bucket
+};
+
+__device__ __forceinline__ void l2_items_init(const HistoArgs& a, L2Items& it)
+{
+    wave0_excl_scan(a.scratch + kOffCnt1, it.off1, kL1Buckets, true);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kL1Buckets; b += blockDim.x) {
+        const uint32_t l = a.scratch[kOffCur1 + b];
+        it.len1[b] = l;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        // istart = exclusive scan of ceil(len1 / chunk)
+        const int lane = threadIdx.x;
+        uint32_t v[5], sum = 0;
+        for (int j = 0; j < 5; j++) {
+            const int i = lane * 5 + j;
+            v[j] = i < kL1Buckets ? (it.len1[i] + kPartChunk - 1) / kPartChunk : 0u;
+            sum += v[j];
+        }
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= o)
+                incl += t;
+        }
+        uint32_t run = incl - sum;
+        for (int j = 0; j < 5; j++) {
+            const int i = lane * 5 + j;
+            if (i <= kL1Buckets)
+                it.istart[i] = run;
+            run += v[j];
+        }
+    }
+    __syncthreads();
+}
+
+// Level 2a: per (bucket, chunk) count keys per slice of the bucket.
+__global__ void __launch_bounds__(kPartThreads) rx_part2_count_kernel(HistoArgs a)
+{
+    __shared__ L2Items it;
+    __shared__ uint32_t lcnt[kSubs];
+    l2_items_init(a, it);
+    const int tid = threadIdx.x;
+    const uint32_t nitems = it.istart[kL1Buckets];
+    uint32_t* cnt2 = a.scratch + kOffCnt2;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const int b = find_run(it.istart, kL1Buckets, item);
+        const uint32_t c0 = (item - it.istart[b]) * (uint32_t)kPartChunk;
+        const uint32_t end = min(it.len1[b], c0 + (uint32_t)kPartChunk);
+        if (tid < kSubs)
+            lcnt[tid] = 0;
+        __syncthreads();
+        const uint32_t* src = a.part1 + it.off1[b];
+        for (uint32_t p = c0 + tid; p < end; p += kPartThreads)
+            atomicAdd(&lcnt[(src[p] >> kSliceBits) & (kSubs - 1)], 1u);
+        __syncthreads();
+        if (tid < kSubs && lcnt[tid])
+            atomicAdd(&cnt2[b * kSubs + tid], lcnt[tid]);
+        __syncthreads();
+    }
+}
+
+// Level 2b: per (bucket, chunk) local sort by slice, runs appended per slice.
+__global__ void __launch_bounds__(kPartThreads) rx_part2_scatter_kernel(HistoArgs a)
+{
+    __shared__ L2Items it;
+    __shared__ uint32_t stage[kPartChunk];
+    __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1], soff[kSubs + 1], gpos[kSubs];
+    l2_items_init(a, it);
+    const int tid = threadIdx.x;
+    const uint32_t nitems = it.istart[kL1Buckets];
+    const uint32_t* cnt2 = a.scratch + kOffCnt2;
+    uint32_t* cur2 = a.scratch + kOffCur2;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const int b = find_run(it.istart, kL1Buckets, item);
+        const uint32_t c0 = (item - it.istart[b]) * (uint32_t)kPartChunk;
+        const uint32_t end = min(it.len1[b], c0 + (uint32_t)kPartChunk);
+        if (tid < kSubs)
+            lcnt[tid] = 0;
+        wave0_excl_scan(cnt2 + b * kSubs, soff, kSubs, true);  // slice starts inside the bucket
+        __syncthreads();
+        const uint32_t* src = a.part1 + it.off1[b];
+        uint32_t key[kPartKeysPerThread], rank[kPartKeysPerThread];
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++) {
+            const uint32_t p = c0 + (uint32_t)(j * kPartThreads + tid);
+            key[j] = p < end ? src[p] : 0u;
+            rank[j] = p < end ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0xffffffffu;
+        }
+        __syncthreads();
+        wave0_excl_scan(lcnt, loff, kSubs, false);
+        if (tid < kSubs && lcnt[tid])
+            gpos[tid] = it.off1[b] + soff[tid] + atomicAdd(&cur2[b * kSubs + tid], lcnt[tid]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            if (rank[j] != 0xffffffffu)
+                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + rank[j]] = key[j];
+        __syncthreads();
+        const uint32_t nkeys = end - c0;
+        for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
+            const int sub = find_run(loff, kSubs, p);
+            a.part2[gpos[sub] + (p - loff[sub])] = stage[p];
+        }
+        __syncthreads();
+    }
+}
+
+// Level 3: one block per 16K-bin slice: LDS histogram of the slice's keys,
+// then one read-modify-write of the slice's table words that received
+// events (16 B per lane, coalesced; untouched 16-B groups are skipped).
+__global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
+    __shared__ uint32_t acc[2];
+    const int tid = threadIdx.x;
+    const uint32_t s = blockIdx.x;
+    const uint32_t len = a.scratch[kOffCnt2 + s];
+    if (len == 0)
+        return;
+    const uint32_t b = s / kSubs, sub = s % kSubs;
+    if (tid < 2)
+        acc[tid] = 0;
+    __syncthreads();
+    // start = off1[b] + sum(cnt2[b*kSubs .. s))
+    uint32_t part = 0;
+    if ((uint32_t)tid < b)
+        part += a.scratch[kOffCnt1 + tid];
+    if (tid >= 300 && (uint32_t)(tid - 300) < sub)
+        part += a.scratch[kOffCnt2 + b * kSubs + (tid - 300)];
+    if (part)
+        atomicAdd(&acc[0], part);
+    u32x4_t* h4 = (u32x4_t*)h;
+    for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads)
+        h4[c] = u32x4_t{0u, 0u, 0u, 0u};
+    __syncthreads();
+    const uint32_t* src = a.part2 + acc[0];
+    for (uint32_t p = tid; p < len; p += kSliceThreads)
+        atomicAdd(&h[src[p] & ((1u << kSliceBits) - 1)], 1u);
+    __syncthreads();
+    u32x4_t* g4 = (u32x4_t*)(a.hist + ((uint64_t)s << kSliceBits));
+    for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads) {
+        const u32x4_t v = h4[c];
+        if (v.x | v.y | v.z | v.w) {
+            u32x4_t g = g4[c];
+            g += v;  // u32 wrap, like the reference's atomic_fetch_add on u32
+            g4[c] = g;
         }
     }
 }

@@ -99,6 +99,10 @@ enum dqdk_gpu_flags {
     DQDK_GPU_F_PREFILTER = 1u << 2,      /* apply the XDP forwarder predicate first     */
     DQDK_GPU_F_NO_HISTO = 1u << 3,       /* decode only, no histogram accumulation      */
     DQDK_GPU_F_CSUM_WRITEBACK = 1u << 4, /* zero udp->check in UMEM like udp.c:17       */
+    /* Histogram accumulation strategy (same table either way; default picks
+     * per batch by event count): */
+    DQDK_GPU_F_HISTO_ATOMIC = 1u << 5,      /* one device atomic per event              */
+    DQDK_GPU_F_HISTO_PARTITIONED = 1u << 6, /* bucket -> slice -> LDS histogram + RMW   */
 };
 
 typedef struct dqdk_gpu_cfg {

@@ -88,7 +88,8 @@ def test_golden_f1_frames(flags):
     if flags & D.F_CSUM:  # reference ip4_audit_checksum is undefined for ihl > 5
         keep = ~((e["ipc_ok"] == 255) & (e["ip_ok"] == 1))
         desc = desc[keep]
-    cfg = D.RxConfig(payloadsz=64, mode=D.MODE_ENERGYHISTO, flags=flags, port_start=0, port_end=65535)
+    cfg = D.RxConfig(payloadsz=64, mode=D.MODE_ENERGYHISTO, flags=flags | D.F_HISTO_PARTITIONED,
+                     port_start=0, port_end=65535)
     ores, _ = compare(umem, desc, cfg, check_hist=True)
     assert len(np.unique(ores["status"])) >= 3
 
@@ -113,10 +114,14 @@ CASES = [
 ]
 
 
+HPATHS = [D.F_HISTO_ATOMIC, D.F_HISTO_PARTITIONED]
+
+
+@pytest.mark.parametrize("hpath", HPATHS, ids=["atomic", "partitioned"])
 @pytest.mark.parametrize("L,stride,faulty,payloadsz,mode,flags", CASES)
-def test_synthetic_parity(L, stride, faulty, payloadsz, mode, flags):
+def test_synthetic_parity(L, stride, faulty, payloadsz, mode, flags, hpath):
     umem, desc = D.synth_umem(3000, L, stride, faulty=faulty)
-    cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags)
+    cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | hpath)
     ores, ocnt = compare(umem, desc, cfg, check_hist=D.histo_enabled(mode, flags))
     assert (ores["status"] == D.RX_OK).mean() > 0.9
 
@@ -129,7 +134,7 @@ def test_unaligned_frames(shift):
     umem[shift:shift + umem0.size] = umem0
     desc = desc.copy()
     desc["addr"] += shift
-    for flags in (0, D.F_CSUM):
+    for flags in (0, D.F_CSUM | D.F_HISTO_PARTITIONED):
         compare(umem, desc, D.RxConfig(payloadsz=1458, flags=flags), check_hist=True)
 
 
@@ -184,8 +189,29 @@ def test_random_bytes_fuzz():
         ul = (tot - ihl * 4) & 0xFFFF
         if u + 8 < umem.size:
             umem[u + 4], umem[u + 5] = ul >> 8, ul & 0xFF
-    for flags in (0, D.F_CSUM, D.F_CSUM | D.F_BATCH_ABORT):
+    for flags in (0, D.F_CSUM | D.F_HISTO_PARTITIONED, D.F_CSUM | D.F_BATCH_ABORT | D.F_HISTO_PARTITIONED):
         compare(umem, desc, D.RxConfig(payloadsz=200, flags=flags), check_hist=True)
+
+
+@pytest.mark.parametrize("hpath", HPATHS, ids=["atomic", "partitioned"])
+def test_skewed_histogram(hpath):
+    """Real spectra are peaked: many events on few bins (LDS/atomic contention,
+    counts far above 1 per bin) and whole buckets empty."""
+    umem, desc = D.synth_umem(4096, 1500, 4096, faulty=False)
+    f = umem.reshape(4096, 4096)
+    rng = np.random.default_rng(5)
+    ev = f[:, 42:42 + 91 * 16].reshape(4096, 91, 16)
+    peaks = np.array([(3, 1, 0x12, 0x34), (3, 1, 0x12, 0x35), (700, 4, 0xff, 0xff), (1511, 5, 0, 0)], np.uint8)
+    pick = rng.integers(0, len(peaks) + 1, size=(4096, 91))
+    for k, (chl, hc, e5, e6) in enumerate(peaks):
+        m = pick == k
+        ev[..., 2][m] = chl & 0xFF if chl < 256 else (chl & 0xFF)
+        ev[..., 3][m] = chl >> 8
+        ev[..., 5][m] = e5
+        ev[..., 6][m] = e6
+        ev[..., 8][m] = hc
+    cfg = D.RxConfig(payloadsz=1458, flags=hpath)  # no checksum: payload edited
+    compare(umem, desc, cfg, check_hist=True)
 
 
 def test_host_dropin_api_matches_device_api():
