@@ -197,7 +197,6 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.keys = keys;
         ha.n = n;
         ha.E = q->E;
-        ha.E_magic = 0xffffffffu / q->E;
         ha.flags = q->cfg.flags;
         ha.batch_scratch = q->d_batch;
         ha.hist = q->d_hist;

@@ -62,7 +62,7 @@ struct RxArgs {
     uint32_t flags;
     uint32_t port_start, port_end;
     uint64_t* batch_scratch;  // [0] = first abort idx, [1..12] = per-batch counters
-    uint32_t* cnt1;           // bucket counts for the partitioned histogram, or null
+    uint32_t* cnt1;           // partitioned histogram: bucket counts (+ KEY_NONE records for non-OK frames), or null
 };
 
 struct CountArgs {
@@ -80,7 +80,6 @@ struct HistoArgs {
     const uint32_t* keys;
     uint32_t n;
     uint32_t E;
-    uint32_t E_magic;  // 0xFFFFFFFF / E (floor), for key index -> frame
     uint32_t flags;
     const uint64_t* batch_scratch;
     uint32_t* hist;

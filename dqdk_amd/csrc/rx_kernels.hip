@@ -219,8 +219,14 @@ __device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& f
     const uint32_t poff = __builtin_amdgcn_readfirstlane(fi_lds.poff);
     const uint32_t hs = __builtin_amdgcn_readfirstlane(fi_lds.hs);
     const uint32_t len16 = __builtin_amdgcn_readfirstlane(fi_lds.len16);
-    const uint32_t E = a.E;
 
+    const uint32_t E = a.E;
+    uint32_t* keys = a.keys + (uint64_t)i * E;
+    if (work == 4) {  // non-OK frame feeding the partitioned histogram: records -> KEY_NONE
+        for (uint32_t e = lane; e < E; e += 64)
+            keys[e] = DQDK_KEY_NONE;
+        return;
+    }
     const uint64_t a0 = addr & ~15ull;
     const int off0 = (int)(addr & 15);
     const bool dec = work & 1, cs = work & 2;
@@ -250,7 +256,6 @@ __device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& f
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + a0), (short)0, nrec, 0x00020000);
 
     uint32_t acc_e = 0, acc_o = 0, oob = 0;
-    uint32_t* keys = a.keys + (uint64_t)i * E;
 
     for (int cb = c_begin; cb < c_end; cb += 64 * kUnroll) {
         u32x4 v[kUnroll];
@@ -333,6 +338,9 @@ __device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& f
             const uint32_t calc = (~f) & 0xffffu;
             if (calc != check)
                 status = DQDK_RX_INVALID_UDP_CSUM;
+            if (status != DQDK_RX_OK && a.cnt1 && a.keys)  // overwrite speculative / absent records
+                for (uint32_t e = lane; e < E; e += 64)
+                    keys[e] = DQDK_KEY_NONE;
             if (lane == 0 && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {
                 uint8_t* ck = const_cast<uint8_t*>(a.umem) + addr + 14 + hs + 6;
                 if (addr + 14 + hs + 8 <= a.umem_size) {
@@ -381,11 +389,18 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
             dqdk_gpu_rx_result_t r;
             bool needB;
             parse_frame(a, i, fi, r, needB);
+            if (!needB) {
+                a.res[i] = r;
+                // the partitioned histogram reads records by index only, so
+                // frames it must skip get KEY_NONE records (rare: non-OK)
+                if (a.cnt1 && a.keys && a.E && r.status != DQDK_RX_OK) {
+                    fi.work = 4;
+                    needB = true;
+                }
+            }
             info[tid] = fi;
             if (needB)
                 work_list[atomicAdd(&work_count, 1)] = tid;
-            else
-                a.res[i] = r;
         }
         __syncthreads();
         const int nw = work_count;
@@ -506,27 +521,6 @@ __device__ __forceinline__ uint32_t frames_limit(const HistoArgs& a)
     return (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (uint32_t)(abort_idx < a.n ? abort_idx : a.n) : a.n;
 }
 
-// key index p -> frame p / E (E_magic = floor(0xFFFFFFFF / E), error <= 2)
-__device__ __forceinline__ uint32_t key_frame(const HistoArgs& a, uint32_t p)
-{
-    uint32_t q = __umulhi(p, a.E_magic);
-    uint32_t r = p - q * a.E;
-    while (r >= a.E) {
-        q++;
-        r -= a.E;
-    }
-    return q;
-}
-
-// the key at index p counts iff its frame is accounted and OK
-__device__ __forceinline__ bool key_counts(const HistoArgs& a, uint32_t p, uint32_t key, uint32_t limit)
-{
-    if (key == DQDK_KEY_NONE)
-        return false;
-    const uint32_t f = key_frame(a, p);
-    return f < limit && a.res[f].status == DQDK_RX_OK;
-}
-
 // Small batches: one relaxed agent-scope atomic per event, one wave per frame.
 __global__ void __launch_bounds__(256) rx_histo_atomic_kernel(HistoArgs a)
 {
@@ -631,7 +625,7 @@ __global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 const uint32_t k = key[4 * j + c];
-                const bool ok = p0 + c < total && key_counts(a, p0 + c, k, limit);
+                const bool ok = p0 + c < total && k != DQDK_KEY_NONE;  // non-OK frames hold KEY_NONE
                 rank[4 * j + c] = ok ? atomicAdd(&lcnt[k >> kL1Shift], 1u) : 0xffffffffu;
             }
         }
@@ -648,8 +642,9 @@ __global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
         __syncthreads();
         const uint32_t nkeys = loff[kL1Buckets];
         for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
-            const int b = find_run(loff, kL1Buckets, p);
-            a.part1[gpos[b] + (p - loff[b])] = stage[p];
+            const uint32_t k = stage[p];
+            const uint32_t b = k >> kL1Shift;
+            a.part1[gpos[b] + (p - loff[b])] = k;
         }
         __syncthreads();
     }
@@ -762,8 +757,9 @@ __global__ void __launch_bounds__(kPartThreads) rx_part2_scatter_kernel(HistoArg
         __syncthreads();
         const uint32_t nkeys = end - c0;
         for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
-            const int sub = find_run(loff, kSubs, p);
-            a.part2[gpos[sub] + (p - loff[sub])] = stage[p];
+            const uint32_t k = stage[p];
+            const uint32_t sub = (k >> kSliceBits) & (kSubs - 1);
+            a.part2[gpos[sub] + (p - loff[sub])] = k;
         }
         __syncthreads();
     }

@@ -201,11 +201,11 @@ def test_skewed_histogram(hpath):
     f = umem.reshape(4096, 4096)
     rng = np.random.default_rng(5)
     ev = f[:, 42:42 + 91 * 16].reshape(4096, 91, 16)
-    peaks = np.array([(3, 1, 0x12, 0x34), (3, 1, 0x12, 0x35), (700, 4, 0xff, 0xff), (1511, 5, 0, 0)], np.uint8)
+    peaks = [(3, 1, 0x12, 0x34), (3, 1, 0x12, 0x35), (700, 4, 0xff, 0xff), (1511, 5, 0, 0)]
     pick = rng.integers(0, len(peaks) + 1, size=(4096, 91))
     for k, (chl, hc, e5, e6) in enumerate(peaks):
         m = pick == k
-        ev[..., 2][m] = chl & 0xFF if chl < 256 else (chl & 0xFF)
+        ev[..., 2][m] = chl & 0xFF
         ev[..., 3][m] = chl >> 8
         ev[..., 5][m] = e5
         ev[..., 6][m] = e6
