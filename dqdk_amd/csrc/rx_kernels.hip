@@ -206,157 +206,250 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
 #undef FB
 }
 
-// ---------------------------------------------------------------------------
-// Phase B: one wave streams one frame.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void stream_frame(const RxArgs& a, const FrameInfo& fi_lds, uint32_t i, int lane,
-                                             uint32_t* lds_cnt1)
+// udp_audit_checksum's verdict from S = sum of the datagram's LE u16 words
+// (check field included as stored): src/tcpip/udp.c:10-20, inet_csum.c:145-216.
+__device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t len16, uint64_t pseudo)
 {
-    // readfirstlane returns int: widen through uint32_t or the low word sign-extends
-    const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fi_lds.addr) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(fi_lds.addr >> 32)) << 32);
-    const uint32_t work = __builtin_amdgcn_readfirstlane(fi_lds.work);
-    const uint32_t poff = __builtin_amdgcn_readfirstlane(fi_lds.poff);
-    const uint32_t hs = __builtin_amdgcn_readfirstlane(fi_lds.hs);
-    const uint32_t len16 = __builtin_amdgcn_readfirstlane(fi_lds.len16);
+    if (len16 >= 7)
+        S -= check;                         // udp->check = 0 before summing (udp.c:17)
+    uint64_t t = (uint64_t)S + pseudo;      // csum_tcpudp_nofold
+    t = (t & 0xffffffffull) + (t >> 32);     // from64to32
+    t = (t & 0xffffffffull) + (t >> 32);
+    uint32_t f = (uint32_t)t;
+    f = (f & 0xffff) + (f >> 16);            // csum_fold
+    f = (f & 0xffff) + (f >> 16);
+    return ((~f) & 0xffffu) == check;
+}
 
-    const uint32_t E = a.E;
-    uint32_t* keys = a.keys + (uint64_t)i * E;
-    if (work == 4) {  // non-OK frame feeding the partitioned histogram: records -> KEY_NONE
-        for (uint32_t e = lane; e < E; e += 64)
-            keys[e] = DQDK_KEY_NONE;
-        return;
-    }
-    const uint64_t a0 = addr & ~15ull;
-    const int off0 = (int)(addr & 15);
-    const bool dec = work & 1, cs = work & 2;
+// ---------------------------------------------------------------------------
+// Phase B: each wave streams its share of the tile's frames as ONE continuous
+// sequence of 1-KiB windows (64 lanes x 16 B, aligned buffer loads), with
+// kRing windows in flight across frame boundaries.  The loop body is
+// straight-line in VMEM terms (every window issues exactly one load and one
+// key store; inactive lanes use out-of-range buffer offsets) so hipcc can
+// count the ring with vmcnt(N) instead of draining it.
+// ---------------------------------------------------------------------------
+constexpr int kRing = 8;
+constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
-    const int dec_lo = off0 + (int)poff;
+struct FrameParams {  // wave-uniform
+    uint64_t addr;
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t work, hs, len16;
+    int cs_lo, cs_hi;
+    int c_begin, c_end, nwin;
+    int ce0, qd, rb;
+    bool dec, cs, need_next;
+};
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes)
+{
+    // SRD from readfirstlane'd halves so hipcc can prove it uniform
+    // (otherwise every buffer op becomes a waterfall loop: guide T20)
+    const uint64_t b = (uint64_t)p;
+    const uint64_t ub = (uint64_t)rfl((uint32_t)b) | ((uint64_t)rfl((uint32_t)(b >> 32)) << 32);
+    const uint32_t nrec = rfl((uint32_t)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)nrec, 0x00020000);
+}
+
+// window extent of a frame (also used by phase A to classify frames)
+__device__ __forceinline__ void frame_ranges(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
+                                             uint32_t E, int& cs_lo, int& cs_hi, int& c_begin, int& c_end,
+                                             int& nwin)
+{
+    const int dec_lo = (int)(off0 + poff);
     const int dec_hi = dec_lo + (int)(16 * E);
-    const int cs_lo = off0 + 14 + (int)hs;
-    const int cs_hi = cs_lo + (int)len16 + (int)(len16 & 1);
+    cs_lo = (int)(off0 + 14 + hs);
+    cs_hi = cs_lo + (int)len16 + (int)(len16 & 1);
     int lo = 0x7fffffff, hi = 0;
-    if (dec) {
+    if (work & 1) {
         lo = dec_lo;
         hi = dec_hi;
     }
-    if (cs) {
+    if (work & 2) {
         lo = min(lo, cs_lo);
         hi = max(hi, cs_hi);
     }
-    const int c_begin = lo >> 4, c_end = (hi + 15) >> 4;
-    const int ce0 = dec_lo >> 4;  // chunk holding event 0
-    const int sft = dec_lo & 15;  // event start within its chunk (uniform)
-    const int qd = (sft + 2) >> 2, rb = (sft + 2) & 3;
-    const bool need_next = sft >= 8;  // bytes sft+2..sft+8 cross into the next chunk
+    c_begin = lo >> 4;
+    c_end = (hi + 15) >> 4;
+    nwin = hi > lo ? (c_end - c_begin + 63) >> 6 : 0;
+}
 
-    uint64_t remain = a.umem_size > a0 ? a.umem_size - a0 : 0;
-    const int nrec = (int)(remain > 0xffffffffull ? 0xffffffffull : remain);
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + a0), (short)0, nrec, 0x00020000);
+__device__ __forceinline__ void frame_params(const RxArgs& a, const FrameInfo& fi, FrameParams& P)
+{
+    // readfirstlane returns int: widen through uint32_t or the low word sign-extends
+    P.addr = (uint64_t)rfl((uint32_t)fi.addr) | ((uint64_t)rfl((uint32_t)(fi.addr >> 32)) << 32);
+    P.work = rfl(fi.work);
+    const uint32_t poff = rfl(fi.poff);
+    P.hs = rfl(fi.hs);
+    P.len16 = rfl(fi.len16);
+    const uint64_t a0 = P.addr & ~15ull;
+    const uint32_t off0 = (uint32_t)(P.addr & 15);
+    P.dec = P.work & 1;
+    P.cs = P.work & 2;
+    frame_ranges(P.work, off0, poff, P.hs, P.len16, a.E, P.cs_lo, P.cs_hi, P.c_begin, P.c_end, P.nwin);
+    const int dec_lo = (int)(off0 + poff);
+    P.ce0 = dec_lo >> 4;             // chunk holding event 0
+    const int sft = dec_lo & 15;     // event start inside its chunk (uniform)
+    P.qd = (sft + 2) >> 2;
+    P.rb = (sft + 2) & 3;
+    P.need_next = sft >= 8;          // bytes sft+2..sft+8 cross into the next chunk
+    P.rsrc = uniform_rsrc(a.umem + a0, a.umem_size > a0 ? a.umem_size - a0 : 0);
+}
 
-    uint32_t acc_e = 0, acc_o = 0, oob = 0;
-
-    for (int cb = c_begin; cb < c_end; cb += 64 * kUnroll) {
-        u32x4 v[kUnroll];
+// One 1-KiB window of frame P: checksum bytes + decode events starting in it.
+__device__ __forceinline__ void process_window(const RxArgs& a, const FrameParams& P, uint32_t slot, int w,
+                                               const u32x4& v, const u32x4& nxt, int lane, bool active,
+                                               __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc_e,
+                                               uint32_t& acc_o, uint32_t& oob, uint32_t* lds_cnt1)
+{
+    const int c = P.c_begin + 64 * w + lane;
+    const bool inr = active && c < P.c_end;
+    if (P.cs) {
+        const int p = c * 16;
+        uint32_t te = 0, to = 0;
 #pragma unroll
-        for (int u = 0; u < kUnroll; u++) {
-            const int c = cb + 64 * u + lane;
-            v[u] = u32x4{0u, 0u, 0u, 0u};
-            if (c < c_end)
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, c * 16, 0, 0);
+        for (int k = 0; k < 4; k++) {
+            const uint32_t wk = (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) &
+                                (inr ? range_mask(p + 4 * k, P.cs_lo, P.cs_hi) : 0u);
+            te += wk & 0x00ff00ffu;
+            to += (wk >> 8) & 0x00ff00ffu;
         }
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) {
-            const int c = cb + 64 * u + lane;
-            if (cb + 64 * u >= c_end)
-                break;
-            if (cs) {
-                const int p = c * 16;
-                uint32_t te = 0, to = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t wk = (k == 0 ? v[u].x : k == 1 ? v[u].y : k == 2 ? v[u].z : v[u].w) &
-                                        range_mask(p + 4 * k, cs_lo, cs_hi);
-                    te += wk & 0x00ff00ffu;
-                    to += (wk >> 8) & 0x00ff00ffu;
-                }
-                acc_e += (te & 0xffff) + (te >> 16);
-                acc_o += (to & 0xffff) + (to >> 16);
+        acc_e += (te & 0xffff) + (te >> 16);
+        acc_o += (to & 0xffff) + (to >> 16);
+    }
+    if (P.dec) {
+        const int e = c - P.ce0;
+        const bool has_evt = inr && e >= 0 && e < (int)a.E;
+        uint32_t n0 = 0, n1 = 0;
+        if (P.need_next) {
+            n0 = __shfl_down(v.x, 1);
+            n1 = __shfl_down(v.y, 1);
+            const uint32_t x0 = rfl(nxt.x), x1 = rfl(nxt.y);  // next window, lane 0
+            if (lane == 63) {
+                n0 = x0;
+                n1 = x1;
             }
-            if (dec) {
-                const int e = c - ce0;
-                const bool has_evt = e >= 0 && e < (int)E && c < c_end;
-                uint32_t n0 = 0, n1 = 0;
-                if (need_next) {
-                    n0 = __shfl_down(v[u].x, 1);
-                    n1 = __shfl_down(v[u].y, 1);
-                    if (lane == 63 && has_evt) {
-                        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (c + 1) * 16, 0, 0);
-                        n0 = t.x;
-                        n1 = t.y;
-                    }
-                }
-                const uint32_t W0 = v[u].x, W1 = v[u].y, W2 = v[u].z, W3 = v[u].w;
-                const uint32_t w0 = qd == 0 ? W0 : qd == 1 ? W1 : qd == 2 ? W2 : qd == 3 ? W3 : n0;
-                const uint32_t w1 = qd == 0 ? W1 : qd == 1 ? W2 : qd == 2 ? W3 : qd == 3 ? n0 : n1;
-                const uint32_t w2 = qd == 0 ? W2 : qd == 1 ? W3 : qd == 2 ? n0 : qd == 3 ? n1 : 0u;
-                const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, rb);  // event bytes 2..5
-                const uint32_t y = __builtin_amdgcn_alignbyte(w2, w1, rb);  // event bytes 6..9
-                const uint32_t ch = x & 0xffffu;
-                const uint32_t bin = (x >> 24) | ((y & 0xffu) << 8);
-                const uint32_t hc = (y >> 16) & 7u;
-                const bool bad = ch >= kChannels || hc >= kHists;
-                const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
-                if (has_evt && a.keys)
-                    keys[e] = key;
-                if (a.cnt1 && has_evt && !bad)
-                    atomicAdd(&lds_cnt1[key >> kL1Shift], 1u);  // capacity of the key's L1 bucket
-                oob += __popcll(__ballot(has_evt && bad));
+        }
+        const int qd = P.qd;
+        const uint32_t W0 = v.x, W1 = v.y, W2 = v.z, W3 = v.w;
+        const uint32_t w0 = qd == 0 ? W0 : qd == 1 ? W1 : qd == 2 ? W2 : qd == 3 ? W3 : n0;
+        const uint32_t w1 = qd == 0 ? W1 : qd == 1 ? W2 : qd == 2 ? W3 : qd == 3 ? n0 : n1;
+        const uint32_t w2 = qd == 0 ? W2 : qd == 1 ? W3 : qd == 2 ? n0 : qd == 3 ? n1 : 0u;
+        const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, P.rb);  // event bytes 2..5
+        const uint32_t y = __builtin_amdgcn_alignbyte(w2, w1, P.rb);  // event bytes 6..9
+        const uint32_t ch = x & 0xffffu;
+        const uint32_t bin = (x >> 24) | ((y & 0xffu) << 8);
+        const uint32_t hc = (y >> 16) & 7u;
+        const bool bad = ch >= kChannels || hc >= kHists;
+        const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
+        // records of this tile live at keys_rsrc + (slot*E + e)*4; one store per window
+        __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + (uint32_t)e) * 4u : kOOB,
+                                              0, 0);
+        if (a.cnt1 && has_evt && !bad)
+            atomicAdd(&lds_cnt1[key >> kL1Shift], 1u);  // capacity of the key's L1 bucket
+        oob += __popcll(__ballot(has_evt && bad));
+    }
+}
+
+// Verdict + result record of one streamed frame (all lanes; uniform branches).
+// Returns the final status.
+__device__ __forceinline__ uint32_t finalize_frame(const RxArgs& a, const FrameInfo& fi, const FrameParams& P,
+                                                   uint32_t frame, int lane, uint32_t acc_e, uint32_t acc_o,
+                                                   uint32_t oob)
+{
+    uint32_t status = rfl(fi.status);
+    if (P.cs) {
+        // udp_csum over [udp, udp + len16 (+1 odd)) relative to the udp start
+        const uint32_t se = wave_sum(acc_e), so = wave_sum(acc_o);
+        const bool even = ((P.addr + 14 + P.hs) & 1) == 0;
+        const uint32_t S = even ? se + 256u * so : so + 256u * se;
+        if (!udp_csum_ok(S, rfl(fi.check), P.len16, fi.pseudo))
+            status = DQDK_RX_INVALID_UDP_CSUM;
+        if (lane == 0 && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {
+            uint8_t* ck = const_cast<uint8_t*>(a.umem) + P.addr + 14 + P.hs + 6;
+            if (P.addr + 14 + P.hs + 8 <= a.umem_size) {
+                ck[0] = 0;
+                ck[1] = 0;
             }
         }
     }
+    if (lane == 0) {
+        dqdk_gpu_rx_result_t r;
+        r.status = (uint8_t)status;
+        const bool ok_or_empty = status == DQDK_RX_OK || status == DQDK_RX_EMPTY;
+        r.datalen = ok_or_empty ? fi.datalen : 0u;
+        r.payload_off = ok_or_empty ? fi.poff : (uint8_t)0;
+        r.oob_events = (uint16_t)(status == DQDK_RX_OK ? min(oob, 0xffffu) : 0u);
+        a.res[frame] = r;
+    }
+    return status;
+}
 
-    if (lane == 0 || cs) {
-        uint32_t status = __builtin_amdgcn_readfirstlane(fi_lds.status);
-        if (cs) {
-            // udp_csum over [udp, udp + len16 (+1 odd)) with check zeroed:
-            // S = sum of LE u16 words relative to the udp start.
-            const uint32_t se = wave_sum(acc_e), so = wave_sum(acc_o);
-            const bool even = ((addr + 14 + hs) & 1) == 0;
-            uint32_t S = even ? se + 256u * so : so + 256u * se;
-            const uint32_t check = __builtin_amdgcn_readfirstlane(fi_lds.check);
-            if (len16 >= 7)
-                S -= check;  // udp->check = 0 before summing (udp.c:17)
-            const uint64_t pseudo = fi_lds.pseudo;
-            uint64_t t = (uint64_t)S + pseudo;           // csum_tcpudp_nofold
-            t = (t & 0xffffffffull) + (t >> 32);          // from64to32
-            t = (t & 0xffffffffull) + (t >> 32);
-            uint32_t f = (uint32_t)t;
-            f = (f & 0xffff) + (f >> 16);                 // csum_fold
-            f = (f & 0xffff) + (f >> 16);
-            const uint32_t calc = (~f) & 0xffffu;
-            if (calc != check)
-                status = DQDK_RX_INVALID_UDP_CSUM;
-            if (status != DQDK_RX_OK && a.cnt1 && a.keys)  // overwrite speculative / absent records
-                for (uint32_t e = lane; e < E; e += 64)
-                    keys[e] = DQDK_KEY_NONE;
-            if (lane == 0 && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {
-                uint8_t* ck = const_cast<uint8_t*>(a.umem) + addr + 14 + hs + 6;
-                if (addr + 14 + hs + 8 <= a.umem_size) {
-                    ck[0] = 0;
-                    ck[1] = 0;
+// The wave's frames are work_list[wave], work_list[wave + kWaves], ... (all
+// with >= 1 window), nwin_total windows in all.  Frames whose checksum fails
+// are appended to fill_list.
+__device__ __forceinline__ void stream_frames(const RxArgs& a, const FrameInfo* info, const int* work_list, int nw_,
+                                              int nwin_total_, uint32_t tile_base, int wave_, int lane,
+                                              __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t* lds_cnt1, int* fill_list,
+                                              int* fill_count)
+{
+    // loop bounds and frame slots are wave-uniform: say so, or hipcc treats
+    // everything derived from them (down to the buffer SRDs) as divergent
+    const int nw = (int)rfl((uint32_t)nw_);
+    const int wave = (int)rfl((uint32_t)wave_);
+    const int total = (int)rfl((uint32_t)nwin_total_);
+    if (total == 0)
+        return;
+    const bool refill = a.cnt1 && a.keys;
+
+    // ---- load cursor: kRing windows ahead of the process cursor ----
+    FrameParams L;
+    int jl = wave, wl = 0;
+    frame_params(a, info[rfl((uint32_t)work_list[jl])], L);
+    auto issue = [&](u32x4& dst) {
+        const int c = L.c_begin + 64 * wl + lane;
+        const bool live = jl < nw && c < L.c_end;
+        dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, live ? (uint32_t)c * 16u : kOOB, 0, 0);
+        if (jl < nw && ++wl == L.nwin) {
+            wl = 0;
+            jl += kWaves;
+            if (jl < nw)
+                frame_params(a, info[rfl((uint32_t)work_list[jl])], L);
+        }
+    };
+    u32x4 buf[kRing];
+#pragma unroll
+    for (int d = 0; d < kRing; d++)
+        issue(buf[d]);
+
+    // ---- process cursor: a fixed-trip loop, one load + one store per window ----
+    FrameParams P;
+    int jp = wave, wp = 0;
+    int slot = (int)rfl((uint32_t)work_list[jp]);
+    frame_params(a, info[slot], P);
+    uint32_t acc_e = 0, acc_o = 0, oob = 0;
+    for (int k = 0; k < total; k += kRing) {
+#pragma unroll
+        for (int d = 0; d < kRing; d++) {
+            const bool active = k + d < total;
+            process_window(a, P, (uint32_t)slot, wp, buf[d], buf[(d + 1) % kRing], lane, active, keys_rsrc, acc_e,
+                           acc_o, oob, lds_cnt1);
+            if (active && ++wp == P.nwin) {
+                const uint32_t st = finalize_frame(a, info[slot], P, tile_base + slot, lane, acc_e, acc_o, oob);
+                if (refill && st != DQDK_RX_OK && lane == 0)
+                    fill_list[atomicAdd(fill_count, 1)] = slot;  // records -> KEY_NONE after the stream
+                acc_e = acc_o = oob = 0;
+                wp = 0;
+                jp += kWaves;
+                if (jp < nw) {
+                    slot = (int)rfl((uint32_t)work_list[jp]);
+                    frame_params(a, info[slot], P);
                 }
             }
-        }
-        if (lane == 0) {
-            dqdk_gpu_rx_result_t r;
-            r.status = (uint8_t)status;
-            const bool ok_or_empty = status == DQDK_RX_OK || status == DQDK_RX_EMPTY;
-            r.datalen = ok_or_empty ? fi_lds.datalen : 0u;
-            r.payload_off = ok_or_empty ? (uint8_t)poff : (uint8_t)0;
-            r.oob_events = (uint16_t)(status == DQDK_RX_OK ? min(oob, 0xffffu) : 0u);
-            a.res[i] = r;
+            issue(buf[d]);
         }
     }
 }
@@ -365,11 +458,16 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 {
     __shared__ FrameInfo info[kTile];
     __shared__ int work_list[kTile];
-    __shared__ int work_count;
+    __shared__ int fill_list[kTile];
+    __shared__ int work_count, fill_count;
+    __shared__ int wave_windows[kWaves];
     __shared__ uint32_t lds_cnt1[kL1Buckets];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
+    // the partitioned histogram reads records by index only: frames it must
+    // skip (every non-OK frame) get KEY_NONE records
+    const bool fill_none = a.cnt1 && a.keys && a.E;
     if (a.cnt1) {
         for (int b = tid; b < kL1Buckets; b += kTile)
             lds_cnt1[b] = 0;
@@ -380,8 +478,12 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        if (tid == 0)
+        if (tid == 0) {
             work_count = 0;
+            fill_count = 0;
+        }
+        if (tid < kWaves)
+            wave_windows[tid] = 0;
         __syncthreads();
         const uint32_t i = t * kTile + tid;
         if (i < a.n) {
@@ -389,24 +491,44 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
             dqdk_gpu_rx_result_t r;
             bool needB;
             parse_frame(a, i, fi, r, needB);
-            if (!needB) {
-                a.res[i] = r;
-                // the partitioned histogram reads records by index only, so
-                // frames it must skip get KEY_NONE records (rare: non-OK)
-                if (a.cnt1 && a.keys && a.E && r.status != DQDK_RX_OK) {
-                    fi.work = 4;
-                    needB = true;
+            int nwin = 0;
+            if (needB) {
+                int cs_lo, cs_hi, c_begin, c_end;
+                frame_ranges(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E, cs_lo, cs_hi,
+                             c_begin, c_end, nwin);
+                if (nwin == 0) {  // checksum over an empty datagram (len16 == 0), nothing to stream
+                    if (!udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))
+                        r.status = DQDK_RX_INVALID_UDP_CSUM;
+                    if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {
+                        r.datalen = 0;
+                        r.payload_off = 0;
+                    }
+                    needB = false;
                 }
             }
             info[tid] = fi;
-            if (needB)
-                work_list[atomicAdd(&work_count, 1)] = tid;
+            if (needB) {
+                const int pos = atomicAdd(&work_count, 1);
+                work_list[pos] = tid;
+                atomicAdd(&wave_windows[pos % kWaves], nwin);  // wave pos % kWaves streams it
+            } else {
+                a.res[i] = r;
+                if (fill_none && r.status != DQDK_RX_OK)
+                    fill_list[atomicAdd(&fill_count, 1)] = tid;
+            }
         }
         __syncthreads();
-        const int nw = work_count;
-        for (int j = wave; j < nw; j += kWaves) {
-            const int slot = work_list[j];
-            stream_frame(a, info[slot], t * kTile + slot, lane, lds_cnt1);
+        const __amdgpu_buffer_rsrc_t keys_rsrc =
+            uniform_rsrc(a.keys + (uint64_t)t * kTile * a.E, a.keys ? (uint64_t)kTile * a.E * 4u : 0u);
+        stream_frames(a, info, work_list, work_count, wave_windows[wave], t * kTile, wave, lane, keys_rsrc,
+                      lds_cnt1, fill_list, &fill_count);
+        __syncthreads();
+        // KEY_NONE records for non-OK frames (rare), outside the streamed loop
+        const int nf = fill_count;
+        for (int j = wave; j < nf; j += kWaves) {
+            uint32_t* k = a.keys + (uint64_t)(t * kTile + fill_list[j]) * a.E;
+            for (uint32_t e = lane; e < a.E; e += 64)
+                k[e] = DQDK_KEY_NONE;
         }
         __syncthreads();
     }
