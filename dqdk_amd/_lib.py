@@ -78,6 +78,7 @@ SIGNATURES = {
     "dqdk_gpu_queue_destroy": (C.c_int, [_P]),
     "dqdk_gpu_queue_set_stream": (C.c_int, [_P, _P]),
     "dqdk_gpu_queue_stream": (_P, [_P]),
+    "dqdk_gpu_queue_own_stream": (_P, [_P]),
     "dqdk_gpu_rx_batch_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, _P]),
     "dqdk_gpu_queue_sync": (C.c_int, [_P]),
     "dqdk_gpu_umem_register": (C.c_int, [_P, _P, C.c_uint64]),

@@ -337,9 +337,11 @@ int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* s)
 {
     if (!q)
         return -EINVAL;
-    q->stream = s ? (hipStream_t)s : q->own_stream;
+    q->stream = (hipStream_t)s;  // verbatim: NULL is the legacy default stream
     return 0;
 }
+
+void* dqdk_gpu_queue_own_stream(dqdk_gpu_queue_t* q) { return q ? (void*)q->own_stream : nullptr; }
 
 void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q) { return q ? (void*)q->stream : nullptr; }
 

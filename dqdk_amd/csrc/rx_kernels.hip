@@ -23,9 +23,55 @@ struct FrameInfo {
     uint16_t check;    // udp->check as stored (LE u16)
     uint8_t status;
     uint8_t poff;      // payload offset from the frame start
-    uint8_t work;      // bit0 decode, bit1 udp checksum pending
+    uint8_t work;      // bit0 decode, bit1 udp checksum pending, 4 = KEY_NONE fill only
     uint8_t hs;        // ihl * 4
 };
+
+// Streaming geometry of one frame, relative to a0 = frame address & ~15.
+// Chunk c covers bytes [16c + q4, 16c + q4 + 16): q4 puts event byte 2 of
+// every event at a fixed dword (offset r) of one lane's chunk, so a lane
+// decodes its event from its own 16 B (no cross-lane shuffles).
+struct Geo {
+    int q4, r, ce0;         // grid shift, byte offset of event byte 2 in its dword, chunk of event 0
+    int c_begin, c_end;     // streamed chunks
+    int nwin;               // 1-KiB windows (64 chunks)
+    int ct;                 // last chunk holding checksum bytes (-1: none)
+    int cs_lo, cs_hi;       // checksum byte range [udp, udp + len16 (+1 odd))
+};
+
+__device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
+                                         uint32_t E)
+{
+    Geo g;
+    const bool dec = work & 1, cs = work & 2;
+    const int dec_lo = (int)(off0 + poff);
+    const int dec_hi = dec_lo + (int)(16 * E);
+    g.cs_lo = (int)(off0 + 14 + hs);
+    g.cs_hi = g.cs_lo + (int)len16 + (int)(len16 & 1);
+    const int q = dec ? ((dec_lo + 2) & ~3) : 0;
+    g.q4 = q & 15;
+    g.r = (dec_lo + 2) & 3;
+    g.ce0 = q >> 4;
+    int lo = 0x7fffffff, hi = 0;
+    if (dec) {
+        lo = dec_lo;
+        hi = dec_hi;
+    }
+    if (cs) {
+        lo = min(lo, g.cs_lo);
+        hi = max(hi, g.cs_hi);
+    }
+    if (hi <= lo) {
+        g.c_begin = g.c_end = g.nwin = 0;
+        g.ct = -1;
+        return g;
+    }
+    g.c_begin = (lo - g.q4) >> 4;  // lo >= 14 > q4
+    g.c_end = (hi - g.q4 + 15) >> 4;
+    g.nwin = (g.c_end - g.c_begin + 63) >> 6;
+    g.ct = (cs && g.cs_hi > g.cs_lo) ? ((g.cs_hi - 1 - g.q4) >> 4) : -1;
+    return g;
+}
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int b) { return (w >> (8 * b)) & 0xffu; }
 
@@ -236,10 +282,8 @@ struct FrameParams {  // wave-uniform
     uint64_t addr;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t work, hs, len16;
-    int cs_lo, cs_hi;
-    int c_begin, c_end, nwin;
-    int ce0, qd, rb;
-    bool dec, cs, need_next;
+    Geo g;
+    bool dec, cs;
 };
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -254,29 +298,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
     return __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)nrec, 0x00020000);
 }
 
-// window extent of a frame (also used by phase A to classify frames)
-__device__ __forceinline__ void frame_ranges(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
-                                             uint32_t E, int& cs_lo, int& cs_hi, int& c_begin, int& c_end,
-                                             int& nwin)
-{
-    const int dec_lo = (int)(off0 + poff);
-    const int dec_hi = dec_lo + (int)(16 * E);
-    cs_lo = (int)(off0 + 14 + hs);
-    cs_hi = cs_lo + (int)len16 + (int)(len16 & 1);
-    int lo = 0x7fffffff, hi = 0;
-    if (work & 1) {
-        lo = dec_lo;
-        hi = dec_hi;
-    }
-    if (work & 2) {
-        lo = min(lo, cs_lo);
-        hi = max(hi, cs_hi);
-    }
-    c_begin = lo >> 4;
-    c_end = (hi + 15) >> 4;
-    nwin = hi > lo ? (c_end - c_begin + 63) >> 6 : 0;
-}
-
 __device__ __forceinline__ void frame_params(const RxArgs& a, const FrameInfo& fi, FrameParams& P)
 {
     // readfirstlane returns int: widen through uint32_t or the low word sign-extends
@@ -285,72 +306,65 @@ __device__ __forceinline__ void frame_params(const RxArgs& a, const FrameInfo& f
     const uint32_t poff = rfl(fi.poff);
     P.hs = rfl(fi.hs);
     P.len16 = rfl(fi.len16);
-    const uint64_t a0 = P.addr & ~15ull;
-    const uint32_t off0 = (uint32_t)(P.addr & 15);
     P.dec = P.work & 1;
     P.cs = P.work & 2;
-    frame_ranges(P.work, off0, poff, P.hs, P.len16, a.E, P.cs_lo, P.cs_hi, P.c_begin, P.c_end, P.nwin);
-    const int dec_lo = (int)(off0 + poff);
-    P.ce0 = dec_lo >> 4;             // chunk holding event 0
-    const int sft = dec_lo & 15;     // event start inside its chunk (uniform)
-    P.qd = (sft + 2) >> 2;
-    P.rb = (sft + 2) & 3;
-    P.need_next = sft >= 8;          // bytes sft+2..sft+8 cross into the next chunk
+    P.g = frame_geo(P.work, (uint32_t)(P.addr & 15), poff, P.hs, P.len16, a.E);
+    const uint64_t a0 = P.addr & ~15ull;
     P.rsrc = uniform_rsrc(a.umem + a0, a.umem_size > a0 ? a.umem_size - a0 : 0);
 }
 
-// One 1-KiB window of frame P: checksum bytes + decode events starting in it.
+// One 1-KiB window of frame P: checksum sums + decode of the events whose
+// byte 2 falls in each lane's chunk.
 __device__ __forceinline__ void process_window(const RxArgs& a, const FrameParams& P, uint32_t slot, int w,
-                                               const u32x4& v, const u32x4& nxt, int lane, bool active,
+                                               const u32x4& v, int lane, bool active,
                                                __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc_e,
                                                uint32_t& acc_o, uint32_t& oob, uint32_t* lds_cnt1)
 {
-    const int c = P.c_begin + 64 * w + lane;
-    const bool inr = active && c < P.c_end;
+    const int c0 = P.g.c_begin + 64 * w;
+    const int c = c0 + lane;
+    const bool inr = active && c < P.g.c_end;
     if (P.cs) {
-        const int p = c * 16;
-        uint32_t te = 0, to = 0;
+        const uint32_t M = 0x00ff00ffu;  // bytes at even positions (chunk starts are 4-aligned)
+        uint32_t te = (v.x & M) + (v.y & M) + (v.z & M) + (v.w & M);
+        uint32_t to = ((v.x >> 8) & M) + ((v.y >> 8) & M) + ((v.z >> 8) & M) + ((v.w >> 8) & M);
+        const bool incs = inr && c <= P.g.ct;
+        te = incs ? te : 0u;
+        to = incs ? to : 0u;
+        if (active && (w == 0 || (P.g.ct >= c0 && P.g.ct < c0 + 64))) {
+            // uniform: this window holds the first or the last checksum chunk;
+            // drop their bytes outside [cs_lo, cs_hi) (the odd-length
+            // over-read byte is inside: cs_hi includes it)
+            const int p = 16 * c + P.g.q4;
+            uint32_t de = 0, dd = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t wk = (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) &
-                                (inr ? range_mask(p + 4 * k, P.cs_lo, P.cs_hi) : 0u);
-            te += wk & 0x00ff00ffu;
-            to += (wk >> 8) & 0x00ff00ffu;
+            for (int k = 0; k < 4; k++) {
+                const uint32_t wk = (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) &
+                                    ~range_mask(p + 4 * k, P.g.cs_lo, P.g.cs_hi);
+                de += wk & M;
+                dd += (wk >> 8) & M;
+            }
+            const bool edge = incs && (c == P.g.c_begin || c == P.g.ct);
+            te -= edge ? de : 0u;
+            to -= edge ? dd : 0u;
         }
         acc_e += (te & 0xffff) + (te >> 16);
         acc_o += (to & 0xffff) + (to >> 16);
     }
     if (P.dec) {
-        const int e = c - P.ce0;
-        const bool has_evt = inr && e >= 0 && e < (int)a.E;
-        uint32_t n0 = 0, n1 = 0;
-        if (P.need_next) {
-            n0 = __shfl_down(v.x, 1);
-            n1 = __shfl_down(v.y, 1);
-            const uint32_t x0 = rfl(nxt.x), x1 = rfl(nxt.y);  // next window, lane 0
-            if (lane == 63) {
-                n0 = x0;
-                n1 = x1;
-            }
-        }
-        const int qd = P.qd;
-        const uint32_t W0 = v.x, W1 = v.y, W2 = v.z, W3 = v.w;
-        const uint32_t w0 = qd == 0 ? W0 : qd == 1 ? W1 : qd == 2 ? W2 : qd == 3 ? W3 : n0;
-        const uint32_t w1 = qd == 0 ? W1 : qd == 1 ? W2 : qd == 2 ? W3 : qd == 3 ? n0 : n1;
-        const uint32_t w2 = qd == 0 ? W2 : qd == 1 ? W3 : qd == 2 ? n0 : qd == 3 ? n1 : 0u;
-        const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, P.rb);  // event bytes 2..5
-        const uint32_t y = __builtin_amdgcn_alignbyte(w2, w1, P.rb);  // event bytes 6..9
+        const uint32_t e = (uint32_t)(c - P.g.ce0);
+        const bool has_evt = inr && e < a.E;
+        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, P.g.r);  // event bytes 2..5
+        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, P.g.r);  // event bytes 6..9
         const uint32_t ch = x & 0xffffu;
-        const uint32_t bin = (x >> 24) | ((y & 0xffu) << 8);
-        const uint32_t hc = (y >> 16) & 7u;
+        const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
+        const uint32_t hc = (y >> 16) & 7u;                                // hist_class:3
         const bool bad = ch >= kChannels || hc >= kHists;
         const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
         // records of this tile live at keys_rsrc + (slot*E + e)*4; one store per window
-        __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + (uint32_t)e) * 4u : kOOB,
-                                              0, 0);
-        if (a.cnt1 && has_evt && !bad)
-            atomicAdd(&lds_cnt1[key >> kL1Shift], 1u);  // capacity of the key's L1 bucket
-        oob += __popcll(__ballot(has_evt && bad));
+        __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + e) * 4u : kOOB, 0, 0);
+        if (a.cnt1)  // capacity of the key's L1 bucket (slot kL1Buckets absorbs the rest)
+            atomicAdd(&lds_cnt1[has_evt && !bad ? (key >> kL1Shift) : (uint32_t)kL1Buckets], 1u);
+        oob += (has_evt && bad) ? 1u : 0u;  // per lane; summed at finalize
     }
 }
 
@@ -358,7 +372,7 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const FrameParam
 // Returns the final status.
 __device__ __forceinline__ uint32_t finalize_frame(const RxArgs& a, const FrameInfo& fi, const FrameParams& P,
                                                    uint32_t frame, int lane, uint32_t acc_e, uint32_t acc_o,
-                                                   uint32_t oob)
+                                                   uint32_t oob_lane)
 {
     uint32_t status = rfl(fi.status);
     if (P.cs) {
@@ -376,6 +390,7 @@ __device__ __forceinline__ uint32_t finalize_frame(const RxArgs& a, const FrameI
             }
         }
     }
+    const uint32_t oob = P.dec ? wave_sum(oob_lane) : 0u;
     if (lane == 0) {
         dqdk_gpu_rx_result_t r;
         r.status = (uint8_t)status;
@@ -410,10 +425,10 @@ __device__ __forceinline__ void stream_frames(const RxArgs& a, const FrameInfo* 
     int jl = wave, wl = 0;
     frame_params(a, info[rfl((uint32_t)work_list[jl])], L);
     auto issue = [&](u32x4& dst) {
-        const int c = L.c_begin + 64 * wl + lane;
-        const bool live = jl < nw && c < L.c_end;
-        dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, live ? (uint32_t)c * 16u : kOOB, 0, 0);
-        if (jl < nw && ++wl == L.nwin) {
+        const int c = L.g.c_begin + 64 * wl + lane;
+        const bool live = jl < nw && c < L.g.c_end;
+        dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, live ? (uint32_t)(16 * c + L.g.q4) : kOOB, 0, 0);
+        if (jl < nw && ++wl == L.g.nwin) {
             wl = 0;
             jl += kWaves;
             if (jl < nw)
@@ -435,9 +450,8 @@ __device__ __forceinline__ void stream_frames(const RxArgs& a, const FrameInfo* 
 #pragma unroll
         for (int d = 0; d < kRing; d++) {
             const bool active = k + d < total;
-            process_window(a, P, (uint32_t)slot, wp, buf[d], buf[(d + 1) % kRing], lane, active, keys_rsrc, acc_e,
-                           acc_o, oob, lds_cnt1);
-            if (active && ++wp == P.nwin) {
+            process_window(a, P, (uint32_t)slot, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, oob, lds_cnt1);
+            if (active && ++wp == P.g.nwin) {
                 const uint32_t st = finalize_frame(a, info[slot], P, tile_base + slot, lane, acc_e, acc_o, oob);
                 if (refill && st != DQDK_RX_OK && lane == 0)
                     fill_list[atomicAdd(fill_count, 1)] = slot;  // records -> KEY_NONE after the stream
@@ -461,7 +475,7 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
     __shared__ int fill_list[kTile];
     __shared__ int work_count, fill_count;
     __shared__ int wave_windows[kWaves];
-    __shared__ uint32_t lds_cnt1[kL1Buckets];
+    __shared__ uint32_t lds_cnt1[kL1Buckets + 1];  // + a dummy slot for masked lanes
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -493,9 +507,7 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
             parse_frame(a, i, fi, r, needB);
             int nwin = 0;
             if (needB) {
-                int cs_lo, cs_hi, c_begin, c_end;
-                frame_ranges(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E, cs_lo, cs_hi,
-                             c_begin, c_end, nwin);
+                nwin = frame_geo(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E).nwin;
                 if (nwin == 0) {  // checksum over an empty datagram (len16 == 0), nothing to stream
                     if (!udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))
                         r.status = DQDK_RX_INVALID_UDP_CSUM;

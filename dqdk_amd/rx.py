@@ -92,8 +92,14 @@ class RxQueue:
     def handle(self):
         return self._h
 
-    def set_stream(self, hip_stream_ptr: int | None) -> None:
-        L.check(L.lib().dqdk_gpu_queue_set_stream(self._h, hip_stream_ptr or None), "set_stream")
+    def set_stream(self, hip_stream_ptr: int) -> None:
+        """Order the queue's work on this hipStream_t (0 = the legacy default
+        stream, which is what torch's default stream reports)."""
+        L.check(L.lib().dqdk_gpu_queue_set_stream(self._h, hip_stream_ptr), "set_stream")
+
+    def use_own_stream(self) -> None:
+        L.check(L.lib().dqdk_gpu_queue_set_stream(self._h, L.lib().dqdk_gpu_queue_own_stream(self._h)),
+                "set_stream")
 
     def sync(self) -> None:
         L.check(L.lib().dqdk_gpu_queue_sync(self._h), "queue_sync")

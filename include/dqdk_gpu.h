@@ -129,9 +129,12 @@ int dqdk_gpu_device_count(void);
  * the queue's device histogram (2.38 GB, zeroed) unless the mode has none. */
 int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_batch, dqdk_gpu_queue_t** out);
 int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q);
-/* Run the queue's work on an existing hipStream_t (NULL = its own stream). */
+/* Queues start on a stream of their own (hipStreamNonBlocking).  Run the
+ * queue's work on the caller's hipStream_t instead -- verbatim, so NULL is
+ * the legacy default stream -- to order it after the caller's producers. */
 int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* hip_stream);
-void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q);
+void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q);     /* current stream     */
+void* dqdk_gpu_queue_own_stream(dqdk_gpu_queue_t* q); /* the queue's own one */
 
 /* ---- device-resident batch (async on the queue stream) ------------------- */
 /* d_umem/d_desc/d_results/d_keys are DEVICE pointers.  d_keys (nullable)

@@ -36,7 +36,7 @@ def run_gpu(umem, desc, cfg: D.RxConfig, keys=True, histogram=False, q=None):
     E = cfg.events
     d_umem = to_dev(umem)
     d_desc = to_dev(desc)
-    d_res = torch.zeros(n * 8, dtype=torch.uint8, device="cuda:0")
+    d_res = torch.full((n * 8,), 0xEE, dtype=torch.uint8, device="cuda:0")  # poison: every result must be written
     d_keys = torch.full((max(n * E, 1),), -1, dtype=torch.int32, device="cuda:0") if keys else None
     stream = torch.cuda.current_stream().cuda_stream
     q.set_stream(stream)
@@ -44,6 +44,8 @@ def run_gpu(umem, desc, cfg: D.RxConfig, keys=True, histogram=False, q=None):
                      d_keys.data_ptr() if keys else None)
     torch.cuda.synchronize()
     res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
+    unwritten = np.flatnonzero(res["status"] == 0xEE)
+    assert len(unwritten) == 0, ("unwritten results", len(unwritten), unwritten[:16])
     cnt = q.counters()
     k = d_keys.cpu().numpy().view(np.uint32)[: n * E] if keys else None
     hist = q.histogram() if histogram else None
@@ -273,9 +275,16 @@ def test_full_size_properties(L, stride, payloadsz):
     assert cnt["invalid_ip_pkts"] == int(((st == D.RX_INVALID_IP) | (st == D.RX_INVALID_IP_CSUM)).sum())
     assert cnt["rcvd_bytes"] == int(res["datalen"][st == D.RX_OK].astype(np.uint64).sum())
     mass = int(hist.astype(np.uint64).sum())
-    assert mass == cnt["total_events"] - cnt["oob_events"]
     kk = keys.reshape(n, E)[st == D.RX_OK]
-    assert int((kk != D.KEY_NONE).sum()) == mass
+    nrec = int((kk != D.KEY_NONE).sum())
+    if nrec != cnt["total_events"] - cnt["oob_events"]:
+        okf = np.flatnonzero(st == D.RX_OK)
+        miss = okf[(keys.reshape(n, E)[okf] == D.KEY_NONE).sum(axis=1) > res["oob_events"][okf]]
+        print("frames missing records:", len(miss), miss[:16], "tiles", np.unique(miss // 256)[:16],
+              "slot%4", np.bincount(miss % 256 % 4, minlength=4))
+        f = miss[0]
+        print("frame", f, "NONE at", np.flatnonzero(keys.reshape(n, E)[f] == D.KEY_NONE)[:64])
+    assert (mass, nrec) == (cnt["total_events"] - cnt["oob_events"],) * 2, (mass, nrec)
     # sample of frames vs the oracle
     rng = np.random.default_rng(3)
     idx = np.sort(rng.choice(n, size=4096, replace=False))
