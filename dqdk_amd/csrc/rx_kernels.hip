@@ -91,13 +91,6 @@ __device__ __forceinline__ uint32_t range_mask(int p, int lo, int hi)
     return ml & mh;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o);
-    return v;
-}
 
 // ---------------------------------------------------------------------------
 // Phase A: one lane parses one frame's headers from 112 B staged in VGPRs.
@@ -268,25 +261,37 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// Phase B: each wave streams its share of the tile's frames as ONE continuous
-// sequence of 1-KiB windows (64 lanes x 16 B, aligned buffer loads), with
-// kRing windows in flight across frame boundaries.  The loop body is
-// straight-line in VMEM terms (every window issues exactly one load and one
-// key store; inactive lanes use out-of-range buffer offsets) so hipcc can
-// count the ring with vmcnt(N) instead of draining it.
+// Each wave owns 64-frame tiles end to end (no block barriers):
+//   phase A  lane l parses frame 64*tile + l (headers staged in VGPRs);
+//   phase B  the wave streams the payloads of its frames that need it as
+//            ONE continuous sequence of 1-KiB windows (64 lanes x 16 B
+//            aligned buffer loads), kRing windows in flight across frame
+//            boundaries; per-frame parameters come from the owning lane
+//            (readlane) and per-frame partial sums go back to it (writelane);
+//   phase C  lane l finishes its own frame: checksum verdict, result record
+//            (coalesced), KEY_NONE records for non-OK frames.
+// The phase-B loop body is straight-line in VMEM terms (one load and one key
+// store per window; inactive lanes use out-of-range buffer offsets) so hipcc
+// can count the ring with vmcnt(N) instead of draining it.
 // ---------------------------------------------------------------------------
 constexpr int kRing = 8;
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
-struct FrameParams {  // wave-uniform
-    uint64_t addr;
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t work, hs, len16;
-    Geo g;
-    bool dec, cs;
-};
-
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// sum over the wave: 4 DPP row shifts, then the four row totals
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    return rdl(x, 15) + rdl(x, 31) + rdl(x, 47) + rdl(x, 63);
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes)
 {
@@ -298,252 +303,245 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
     return __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)nrec, 0x00020000);
 }
 
-__device__ __forceinline__ void frame_params(const RxArgs& a, const FrameInfo& fi, FrameParams& P)
+// Per-lane (per-frame) streaming state kept in VGPRs of the owning lane.
+struct LaneFrame {
+    uint32_t addr_lo, addr_hi;
+    uint32_t work;       // bit0 decode, bit1 checksum
+    Geo g;
+};
+
+// Wave-uniform view of one frame (read from its owning lane).
+struct WaveFrame {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t work;
+    int q4, r, ce0, c_begin, c_end, nwin, ct, cs_lo, cs_hi;
+};
+
+__device__ __forceinline__ void wave_frame(const RxArgs& a, const LaneFrame& lf, uint32_t lane_j, bool need_rsrc,
+                                           WaveFrame& W)
 {
-    // readfirstlane returns int: widen through uint32_t or the low word sign-extends
-    P.addr = (uint64_t)rfl((uint32_t)fi.addr) | ((uint64_t)rfl((uint32_t)(fi.addr >> 32)) << 32);
-    P.work = rfl(fi.work);
-    const uint32_t poff = rfl(fi.poff);
-    P.hs = rfl(fi.hs);
-    P.len16 = rfl(fi.len16);
-    P.dec = P.work & 1;
-    P.cs = P.work & 2;
-    P.g = frame_geo(P.work, (uint32_t)(P.addr & 15), poff, P.hs, P.len16, a.E);
-    const uint64_t a0 = P.addr & ~15ull;
-    P.rsrc = uniform_rsrc(a.umem + a0, a.umem_size > a0 ? a.umem_size - a0 : 0);
+    W.work = rdl(lf.work, lane_j);
+    W.q4 = (int)rdl((uint32_t)lf.g.q4, lane_j);
+    W.c_begin = (int)rdl((uint32_t)lf.g.c_begin, lane_j);
+    W.c_end = (int)rdl((uint32_t)lf.g.c_end, lane_j);
+    W.nwin = (int)rdl((uint32_t)lf.g.nwin, lane_j);
+    if (need_rsrc) {
+        const uint64_t addr = (uint64_t)rdl(lf.addr_lo, lane_j) | ((uint64_t)rdl(lf.addr_hi, lane_j) << 32);
+        const uint64_t a0 = addr & ~15ull;
+        W.rsrc = uniform_rsrc(a.umem + a0, a.umem_size > a0 ? a.umem_size - a0 : 0);
+    } else {
+        W.r = (int)rdl((uint32_t)lf.g.r, lane_j);
+        W.ce0 = (int)rdl((uint32_t)lf.g.ce0, lane_j);
+        W.ct = (int)rdl((uint32_t)lf.g.ct, lane_j);
+        W.cs_lo = (int)rdl((uint32_t)lf.g.cs_lo, lane_j);
+        W.cs_hi = (int)rdl((uint32_t)lf.g.cs_hi, lane_j);
+    }
 }
 
-// One 1-KiB window of frame P: checksum sums + decode of the events whose
-// byte 2 falls in each lane's chunk.
-__device__ __forceinline__ void process_window(const RxArgs& a, const FrameParams& P, uint32_t slot, int w,
+// One 1-KiB window of frame P (owned by lane `slot`): checksum sums + decode
+// of the events whose byte 2 falls in each lane's chunk.
+__device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame& P, uint32_t slot, int w,
                                                const u32x4& v, int lane, bool active,
                                                __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc_e,
                                                uint32_t& acc_o, uint32_t& oob, uint32_t* lds_cnt1)
 {
-    const int c0 = P.g.c_begin + 64 * w;
+    const int c0 = P.c_begin + 64 * w;
     const int c = c0 + lane;
-    const bool inr = active && c < P.g.c_end;
-    if (P.cs) {
+    const bool inr = active && c < P.c_end;
+    if (P.work & 2) {
         const uint32_t M = 0x00ff00ffu;  // bytes at even positions (chunk starts are 4-aligned)
         uint32_t te = (v.x & M) + (v.y & M) + (v.z & M) + (v.w & M);
         uint32_t to = ((v.x >> 8) & M) + ((v.y >> 8) & M) + ((v.z >> 8) & M) + ((v.w >> 8) & M);
-        const bool incs = inr && c <= P.g.ct;
+        const bool incs = inr && c <= P.ct;
         te = incs ? te : 0u;
         to = incs ? to : 0u;
-        if (active && (w == 0 || (P.g.ct >= c0 && P.g.ct < c0 + 64))) {
+        if (active && (w == 0 || (P.ct >= c0 && P.ct < c0 + 64))) {
             // uniform: this window holds the first or the last checksum chunk;
-            // drop their bytes outside [cs_lo, cs_hi) (the odd-length
-            // over-read byte is inside: cs_hi includes it)
-            const int p = 16 * c + P.g.q4;
+            // drop their bytes outside [cs_lo, cs_hi) (cs_hi includes the
+            // odd-length over-read byte)
+            const int p = 16 * c + P.q4;
             uint32_t de = 0, dd = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const uint32_t wk = (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) &
-                                    ~range_mask(p + 4 * k, P.g.cs_lo, P.g.cs_hi);
+                                    ~range_mask(p + 4 * k, P.cs_lo, P.cs_hi);
                 de += wk & M;
                 dd += (wk >> 8) & M;
             }
-            const bool edge = incs && (c == P.g.c_begin || c == P.g.ct);
+            const bool edge = incs && (c == P.c_begin || c == P.ct);
             te -= edge ? de : 0u;
             to -= edge ? dd : 0u;
         }
         acc_e += (te & 0xffff) + (te >> 16);
         acc_o += (to & 0xffff) + (to >> 16);
     }
-    if (P.dec) {
-        const uint32_t e = (uint32_t)(c - P.g.ce0);
+    if (P.work & 1) {
+        const uint32_t e = (uint32_t)(c - P.ce0);
         const bool has_evt = inr && e < a.E;
-        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, P.g.r);  // event bytes 2..5
-        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, P.g.r);  // event bytes 6..9
+        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, P.r);  // event bytes 2..5
+        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, P.r);  // event bytes 6..9
         const uint32_t ch = x & 0xffffu;
         const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
         const uint32_t hc = (y >> 16) & 7u;                                // hist_class:3
         const bool bad = ch >= kChannels || hc >= kHists;
         const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
-        // records of this tile live at keys_rsrc + (slot*E + e)*4; one store per window
+        // records of this wave tile live at keys_rsrc + (slot*E + e)*4; one store per window
         __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + e) * 4u : kOOB, 0, 0);
         if (a.cnt1)  // capacity of the key's L1 bucket (slot kL1Buckets absorbs the rest)
             atomicAdd(&lds_cnt1[has_evt && !bad ? (key >> kL1Shift) : (uint32_t)kL1Buckets], 1u);
-        oob += (has_evt && bad) ? 1u : 0u;  // per lane; summed at finalize
+        oob += (has_evt && bad) ? 1u : 0u;  // per lane; summed at the frame's end
     }
 }
 
-// Verdict + result record of one streamed frame (all lanes; uniform branches).
-// Returns the final status.
-__device__ __forceinline__ uint32_t finalize_frame(const RxArgs& a, const FrameInfo& fi, const FrameParams& P,
-                                                   uint32_t frame, int lane, uint32_t acc_e, uint32_t acc_o,
-                                                   uint32_t oob_lane)
+__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t* lds_cnt1)
 {
-    uint32_t status = rfl(fi.status);
-    if (P.cs) {
-        // udp_csum over [udp, udp + len16 (+1 odd)) relative to the udp start
-        const uint32_t se = wave_sum(acc_e), so = wave_sum(acc_o);
-        const bool even = ((P.addr + 14 + P.hs) & 1) == 0;
-        const uint32_t S = even ? se + 256u * so : so + 256u * se;
-        if (!udp_csum_ok(S, rfl(fi.check), P.len16, fi.pseudo))
-            status = DQDK_RX_INVALID_UDP_CSUM;
-        if (lane == 0 && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {
-            uint8_t* ck = const_cast<uint8_t*>(a.umem) + P.addr + 14 + P.hs + 6;
-            if (P.addr + 14 + P.hs + 8 <= a.umem_size) {
-                ck[0] = 0;
-                ck[1] = 0;
-            }
-        }
+    const uint32_t i = tile * 64 + lane;
+    const bool live = i < a.n;
+
+    // ---- phase A: lane parses frame i ----
+    FrameInfo fi;
+    dqdk_gpu_rx_result_t r;
+    bool needB = false;
+    LaneFrame lf;
+    if (live)
+        parse_frame(a, i, fi, r, needB);
+    bool stream = false;
+    if (needB) {
+        lf.g = frame_geo(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E);
+        stream = lf.g.nwin > 0;
+        if (!stream && !udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))  // empty datagram checksum
+            r.status = DQDK_RX_INVALID_UDP_CSUM;
+    } else {
+        lf.g = frame_geo(0, 0, 0, 0, 0, 0);
     }
-    const uint32_t oob = P.dec ? wave_sum(oob_lane) : 0u;
-    if (lane == 0) {
-        dqdk_gpu_rx_result_t r;
-        r.status = (uint8_t)status;
-        const bool ok_or_empty = status == DQDK_RX_OK || status == DQDK_RX_EMPTY;
-        r.datalen = ok_or_empty ? fi.datalen : 0u;
-        r.payload_off = ok_or_empty ? fi.poff : (uint8_t)0;
-        r.oob_events = (uint16_t)(status == DQDK_RX_OK ? min(oob, 0xffffu) : 0u);
-        a.res[frame] = r;
-    }
-    return status;
-}
+    lf.addr_lo = (uint32_t)fi.addr;
+    lf.addr_hi = (uint32_t)(fi.addr >> 32);
+    lf.work = stream ? fi.work : 0u;
 
-// The wave's frames are work_list[wave], work_list[wave + kWaves], ... (all
-// with >= 1 window), nwin_total windows in all.  Frames whose checksum fails
-// are appended to fill_list.
-__device__ __forceinline__ void stream_frames(const RxArgs& a, const FrameInfo* info, const int* work_list, int nw_,
-                                              int nwin_total_, uint32_t tile_base, int wave_, int lane,
-                                              __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t* lds_cnt1, int* fill_list,
-                                              int* fill_count)
-{
-    // loop bounds and frame slots are wave-uniform: say so, or hipcc treats
-    // everything derived from them (down to the buffer SRDs) as divergent
-    const int nw = (int)rfl((uint32_t)nw_);
-    const int wave = (int)rfl((uint32_t)wave_);
-    const int total = (int)rfl((uint32_t)nwin_total_);
-    if (total == 0)
-        return;
-    const bool refill = a.cnt1 && a.keys;
-
-    // ---- load cursor: kRing windows ahead of the process cursor ----
-    FrameParams L;
-    int jl = wave, wl = 0;
-    frame_params(a, info[rfl((uint32_t)work_list[jl])], L);
-    auto issue = [&](u32x4& dst) {
-        const int c = L.g.c_begin + 64 * wl + lane;
-        const bool live = jl < nw && c < L.g.c_end;
-        dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, live ? (uint32_t)(16 * c + L.g.q4) : kOOB, 0, 0);
-        if (jl < nw && ++wl == L.g.nwin) {
-            wl = 0;
-            jl += kWaves;
-            if (jl < nw)
-                frame_params(a, info[rfl((uint32_t)work_list[jl])], L);
-        }
-    };
-    u32x4 buf[kRing];
-#pragma unroll
-    for (int d = 0; d < kRing; d++)
-        issue(buf[d]);
-
-    // ---- process cursor: a fixed-trip loop, one load + one store per window ----
-    FrameParams P;
-    int jp = wave, wp = 0;
-    int slot = (int)rfl((uint32_t)work_list[jp]);
-    frame_params(a, info[slot], P);
-    uint32_t acc_e = 0, acc_o = 0, oob = 0;
-    for (int k = 0; k < total; k += kRing) {
-#pragma unroll
-        for (int d = 0; d < kRing; d++) {
-            const bool active = k + d < total;
-            process_window(a, P, (uint32_t)slot, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, oob, lds_cnt1);
-            if (active && ++wp == P.g.nwin) {
-                const uint32_t st = finalize_frame(a, info[slot], P, tile_base + slot, lane, acc_e, acc_o, oob);
-                if (refill && st != DQDK_RX_OK && lane == 0)
-                    fill_list[atomicAdd(fill_count, 1)] = slot;  // records -> KEY_NONE after the stream
-                acc_e = acc_o = oob = 0;
-                wp = 0;
-                jp += kWaves;
-                if (jp < nw) {
-                    slot = (int)rfl((uint32_t)work_list[jp]);
-                    frame_params(a, info[slot], P);
+    // ---- phase B: stream the payloads ----
+    uint32_t sum_e = 0, sum_o = 0, sum_oob = 0;  // this lane's frame, written by the owner loop
+    const uint64_t smask0 = __ballot(stream);
+    if (smask0) {
+        const int total = (int)wave_sum_dpp(stream ? (uint32_t)lf.g.nwin : 0u);
+        const __amdgpu_buffer_rsrc_t keys_rsrc =
+            uniform_rsrc(a.keys + (uint64_t)tile * 64 * a.E, a.keys ? (uint64_t)64 * a.E * 4u : 0u);
+        // load cursor
+        uint64_t lmask = smask0;
+        uint32_t jl = (uint32_t)__builtin_ctzll(lmask);
+        int wl = 0;
+        WaveFrame L;
+        wave_frame(a, lf, jl, true, L);
+        auto issue = [&](u32x4& dst) {
+            const int c = L.c_begin + 64 * wl + lane;
+            const bool ok = lmask != 0 && c < L.c_end;
+            dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, ok ? (uint32_t)(16 * c + L.q4) : kOOB, 0, 0);
+            if (lmask != 0 && ++wl == L.nwin) {
+                wl = 0;
+                lmask &= lmask - 1;
+                if (lmask) {
+                    jl = (uint32_t)__builtin_ctzll(lmask);
+                    wave_frame(a, lf, jl, true, L);
                 }
             }
+        };
+        u32x4 buf[kRing];
+#pragma unroll
+        for (int d = 0; d < kRing; d++)
             issue(buf[d]);
+        // process cursor
+        uint64_t pmask = smask0;
+        uint32_t jp = (uint32_t)__builtin_ctzll(pmask);
+        int wp = 0;
+        WaveFrame P;
+        wave_frame(a, lf, jp, false, P);
+        uint32_t acc_e = 0, acc_o = 0, oob = 0;
+        for (int k = 0; k < total; k += kRing) {
+#pragma unroll
+            for (int d = 0; d < kRing; d++) {
+                const bool active = k + d < total;
+                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, oob, lds_cnt1);
+                if (active && ++wp == P.nwin) {
+                    // hand the frame's totals to its owning lane
+                    const bool owner = lane == (int)jp;
+                    if (P.work & 2) {
+                        const uint32_t se = wave_sum_dpp(acc_e), so = wave_sum_dpp(acc_o);
+                        sum_e = owner ? se : sum_e;
+                        sum_o = owner ? so : sum_o;
+                    }
+                    if (P.work & 1) {
+                        const uint32_t so = wave_sum_dpp(oob);
+                        sum_oob = owner ? so : sum_oob;
+                    }
+                    acc_e = acc_o = oob = 0;
+                    wp = 0;
+                    pmask &= pmask - 1;
+                    if (pmask) {
+                        jp = (uint32_t)__builtin_ctzll(pmask);
+                        wave_frame(a, lf, jp, false, P);
+                    }
+                }
+                issue(buf[d]);
+            }
+        }
+    }
+
+    // ---- phase C: lane finishes its own frame ----
+    if (stream) {
+        if (fi.work & 2) {
+            // udp_csum over [udp, udp + len16 (+1 odd)) relative to the udp start
+            const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
+            const uint32_t S = even ? sum_e + 256u * sum_o : sum_o + 256u * sum_e;
+            if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
+                r.status = DQDK_RX_INVALID_UDP_CSUM;
+        }
+        r.oob_events = (uint16_t)(r.status == DQDK_RX_OK ? min(sum_oob, 0xffffu) : 0u);
+    }
+    if (live) {
+        if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {
+            r.datalen = 0;
+            r.payload_off = 0;
+        }
+        a.res[i] = r;
+        if ((fi.work & 2) && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {  // udp.c:17 side effect
+            const uint64_t ck = fi.addr + 14 + fi.hs + 6;
+            if (ck + 2 <= a.umem_size) {
+                uint8_t* p = const_cast<uint8_t*>(a.umem) + ck;
+                p[0] = 0;
+                p[1] = 0;
+            }
+        }
+    }
+    // the partitioned histogram reads records by index only: every non-OK
+    // frame gets KEY_NONE records (rare; after this wave's speculative stores)
+    const bool fill = live && a.cnt1 && a.keys && a.E && r.status != DQDK_RX_OK;
+    if (__ballot(fill)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (fill) {
+            uint32_t* k = a.keys + (uint64_t)i * a.E;
+            for (uint32_t e = 0; e < a.E; e++)
+                k[e] = DQDK_KEY_NONE;
         }
     }
 }
 
 __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 {
-    __shared__ FrameInfo info[kTile];
-    __shared__ int work_list[kTile];
-    __shared__ int fill_list[kTile];
-    __shared__ int work_count, fill_count;
-    __shared__ int wave_windows[kWaves];
     __shared__ uint32_t lds_cnt1[kL1Buckets + 1];  // + a dummy slot for masked lanes
-
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    // the partitioned histogram reads records by index only: frames it must
-    // skip (every non-OK frame) get KEY_NONE records
-    const bool fill_none = a.cnt1 && a.keys && a.E;
+    const int lane = tid & 63;
+    const uint32_t wave = rfl((uint32_t)(tid >> 6));
     if (a.cnt1) {
-        for (int b = tid; b < kL1Buckets; b += kTile)
+        for (int b = tid; b < kL1Buckets + 1; b += kTile)
             lds_cnt1[b] = 0;
+        __syncthreads();
     }
-
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
 
-    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        if (tid == 0) {
-            work_count = 0;
-            fill_count = 0;
-        }
-        if (tid < kWaves)
-            wave_windows[tid] = 0;
-        __syncthreads();
-        const uint32_t i = t * kTile + tid;
-        if (i < a.n) {
-            FrameInfo fi;
-            dqdk_gpu_rx_result_t r;
-            bool needB;
-            parse_frame(a, i, fi, r, needB);
-            int nwin = 0;
-            if (needB) {
-                nwin = frame_geo(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E).nwin;
-                if (nwin == 0) {  // checksum over an empty datagram (len16 == 0), nothing to stream
-                    if (!udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))
-                        r.status = DQDK_RX_INVALID_UDP_CSUM;
-                    if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {
-                        r.datalen = 0;
-                        r.payload_off = 0;
-                    }
-                    needB = false;
-                }
-            }
-            info[tid] = fi;
-            if (needB) {
-                const int pos = atomicAdd(&work_count, 1);
-                work_list[pos] = tid;
-                atomicAdd(&wave_windows[pos % kWaves], nwin);  // wave pos % kWaves streams it
-            } else {
-                a.res[i] = r;
-                if (fill_none && r.status != DQDK_RX_OK)
-                    fill_list[atomicAdd(&fill_count, 1)] = tid;
-            }
-        }
-        __syncthreads();
-        const __amdgpu_buffer_rsrc_t keys_rsrc =
-            uniform_rsrc(a.keys + (uint64_t)t * kTile * a.E, a.keys ? (uint64_t)kTile * a.E * 4u : 0u);
-        stream_frames(a, info, work_list, work_count, wave_windows[wave], t * kTile, wave, lane, keys_rsrc,
-                      lds_cnt1, fill_list, &fill_count);
-        __syncthreads();
-        // KEY_NONE records for non-OK frames (rare), outside the streamed loop
-        const int nf = fill_count;
-        for (int j = wave; j < nf; j += kWaves) {
-            uint32_t* k = a.keys + (uint64_t)(t * kTile + fill_list[j]) * a.E;
-            for (uint32_t e = lane; e < a.E; e += 64)
-                k[e] = DQDK_KEY_NONE;
-        }
-        __syncthreads();
-    }
+    const uint32_t ntiles = (a.n + 63) / 64;
+    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves)
+        decode_wave_tile(a, t, lane, lds_cnt1);
+
     if (a.cnt1) {
         __syncthreads();
         for (int b = tid; b < kL1Buckets; b += kTile)
