@@ -82,7 +82,8 @@ struct dqdk_gpu_queue {
     uint64_t* d_batch = nullptr;
     uint32_t* d_keys = nullptr;
     uint32_t* d_part1 = nullptr;   // partitioned-histogram staging (max_batch * E each)
-    uint32_t* d_part2 = nullptr;
+    uint16_t* d_part2 = nullptr;
+    uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     dqdk_gpu_desc_t* d_desc = nullptr;
@@ -165,7 +166,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     const bool partitioned = q->histo && q->E && use_partitioned(q, n);
     ra.cnt1 = partitioned ? q->d_hscratch + kOffCnt1 : nullptr;
     if (partitioned)
-        HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kHistScratchWords * sizeof(uint32_t), q->stream));
+        HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t grid_dec = std::min<uint32_t>(ntiles, (uint32_t)q->cu_count * 8u);
@@ -203,6 +204,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.scratch = q->d_hscratch;
         ha.part1 = q->d_part1;
         ha.part2 = q->d_part2;
+        ha.runs = q->d_runs;
         StageTimer t(q, 2);
         if (!partitioned) {
             const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
@@ -213,8 +215,8 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             const uint32_t grid_p = std::min<uint32_t>(chunks, (uint32_t)q->cu_count * 2u);
             const uint32_t grid_l2 = std::min<uint32_t>(chunks + kL1Buckets, (uint32_t)q->cu_count * 2u);
             hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kPartThreads), 0, q->stream, ha);
-            hipLaunchKernelGGL(rx_part2_count_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
-            hipLaunchKernelGGL(rx_part2_scatter_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+            hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(64), 0, q->stream, ha);
+            hipLaunchKernelGGL(rx_part2_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
             hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
         }
         HIPCHK(hipGetLastError());
@@ -292,9 +294,11 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
-            const size_t kb = (size_t)max_batch * q->E * sizeof(uint32_t);
-            if ((e = hipMalloc(&q->d_keys, kb)) != hipSuccess || (e = hipMalloc(&q->d_part1, kb)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part2, kb)) != hipSuccess ||
+            const size_t nk = (size_t)max_batch * q->E;
+            const size_t items = nk / kPartChunk + kL1Buckets + 1;
+            if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess || (e = hipMalloc(&q->d_part1, nk * 4)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part2, nk * 2)) != hipSuccess ||
+                (e = hipMalloc(&q->d_runs, items * kItemOffs * sizeof(uint16_t))) != hipSuccess ||
                 (e = hipMalloc(&q->d_hscratch, kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
         }
@@ -324,6 +328,7 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_keys);
     (void)hipFree(q->d_part1);
     (void)hipFree(q->d_part2);
+    (void)hipFree(q->d_runs);
     (void)hipFree(q->d_hscratch);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);

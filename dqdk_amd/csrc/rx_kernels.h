@@ -15,11 +15,12 @@
  * K3 histogram accumulation of the keys of accounted OK frames (the relaxed
  *    atomic increment of src/tristan.c:243), two interchangeable forms:
  *    - rx_histo_atomic: one device-scope atomic per event (small batches);
- *    - partitioned: rx_part1 (keys -> 284 buckets of 2^21 bins),
- *      rx_part2_count / rx_part2_scatter (bucket -> 16K-bin slices),
- *      rx_slice_histo (LDS histogram per slice + one coalesced
- *      read-modify-write of the slice's 64 KB of table).  Same multiset of
- *      increments, so the table is bit-identical.
+ *    - partitioned: rx_part1 (keys -> 284 buckets of 2^21 bins, long runs),
+ *      rx_part2 (each 16K-key chunk of a bucket sorted by 16K-bin slice in
+ *      LDS, written back as u16 slice-local keys + run offsets),
+ *      rx_slice_histo (gathers the slice's runs, LDS histogram, one
+ *      coalesced read-modify-write of the slice's 64 KB of table).  Same
+ *      multiset of increments, so the table is bit-identical.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -44,12 +45,14 @@ constexpr int kPartKeysPerThread = 16;
 constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 16384 keys staged in LDS
 constexpr int kSliceThreads = 512;
 
-// u32 scratch words used by the partitioned histogram (zeroed per batch)
-constexpr int kOffCnt1 = 0;                   // [kL1Buckets] keys per bucket (decode, upper bound)
-constexpr int kOffCur1 = 288;                 // [kL1Buckets] keys written per bucket (part1)
-constexpr int kOffCnt2 = 576;                 // [kSlices]    keys per slice (part2_count)
-constexpr int kOffCur2 = kOffCnt2 + kSlices;  // [kSlices]    append cursors (part2_scatter)
-constexpr int kHistScratchWords = kOffCur2 + kSlices;
+// u32 scratch words used by the partitioned histogram
+constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket (decode; upper bound)  -- zeroed per batch
+constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket (part1 cursors)   -- zeroed per batch
+constexpr int kZeroWords = 576;
+constexpr int kOffOff1 = 576;       // [kL1Buckets + 1] bucket starts in part1/part2 (prep)
+constexpr int kOffIstart = 864;     // [kL1Buckets + 1] first part2 item of each bucket (prep)
+constexpr int kHistScratchWords = 1152;
+constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a bucket)
 
 struct RxArgs {
     const uint8_t* umem;
@@ -84,8 +87,9 @@ struct HistoArgs {
     const uint64_t* batch_scratch;
     uint32_t* hist;
     uint32_t* scratch;  // kHistScratchWords
-    uint32_t* part1;    // n*E
-    uint32_t* part2;    // n*E
+    uint32_t* part1;    // n*E keys grouped by bucket
+    uint16_t* part2;    // n*E slice-local keys (key & 16383), each 16K chunk of a bucket sorted by slice
+    uint16_t* runs;     // [items][kItemOffs] slice run starts inside each chunk
 };
 
 __global__ void rx_decode_kernel(RxArgs a);
@@ -93,8 +97,8 @@ __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);
 __global__ void rx_part1_kernel(HistoArgs a);
-__global__ void rx_part2_count_kernel(HistoArgs a);
-__global__ void rx_part2_scatter_kernel(HistoArgs a);
+__global__ void rx_hist_prep_kernel(HistoArgs a);
+__global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);
 
 }  // namespace dqdk

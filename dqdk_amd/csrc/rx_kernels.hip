@@ -782,162 +782,129 @@ __global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
     }
 }
 
-// Work items of level 2: (bucket, 16K-key chunk of the bucket's part1 run).
-struct L2Items {
-    uint32_t off1[kL1Buckets + 1];   // bucket start in part1/part2
-    uint32_t len1[kL1Buckets];       // keys written by part1
-    uint32_t istart[kL1Buckets + 1]; // first item of each bucket
-};
-
-__device__ __forceinline__ void l2_items_init(const HistoArgs& a, L2Items& it)
+// Bucket starts (scan of the decode's upper bounds) and part2 item starts
+// (scan of ceil(bucket length / chunk)), once per batch.
+__global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 {
-    wave0_excl_scan(a.scratch + kOffCnt1, it.off1, kL1Buckets, true);
-    __syncthreads();
-    for (int b = threadIdx.x; b < kL1Buckets; b += blockDim.x) {
-        const uint32_t l = a.scratch[kOffCur1 + b];
-        it.len1[b] = l;
+    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true);
+    const int lane = threadIdx.x;
+    uint32_t v[5], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const int i = lane * 5 + j;
+        v[j] = i < kL1Buckets ? (a.scratch[kOffCur1 + i] + kPartChunk - 1) / kPartChunk : 0u;
+        sum += v[j];
     }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        // istart = exclusive scan of ceil(len1 / chunk)
-        const int lane = threadIdx.x;
-        uint32_t v[5], sum = 0;
-        for (int j = 0; j < 5; j++) {
-            const int i = lane * 5 + j;
-            v[j] = i < kL1Buckets ? (it.len1[i] + kPartChunk - 1) / kPartChunk : 0u;
-            sum += v[j];
-        }
-        uint32_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= o)
-                incl += t;
-        }
-        uint32_t run = incl - sum;
-        for (int j = 0; j < 5; j++) {
-            const int i = lane * 5 + j;
-            if (i <= kL1Buckets)
-                it.istart[i] = run;
-            run += v[j];
-        }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o)
+            incl += t;
     }
-    __syncthreads();
-}
-
-// Level 2a: per (bucket, chunk) count keys per slice of the bucket.
-__global__ void __launch_bounds__(kPartThreads) rx_part2_count_kernel(HistoArgs a)
-{
-    __shared__ L2Items it;
-    __shared__ uint32_t lcnt[kSubs];
-    l2_items_init(a, it);
-    const int tid = threadIdx.x;
-    const uint32_t nitems = it.istart[kL1Buckets];
-    uint32_t* cnt2 = a.scratch + kOffCnt2;
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const int b = find_run(it.istart, kL1Buckets, item);
-        const uint32_t c0 = (item - it.istart[b]) * (uint32_t)kPartChunk;
-        const uint32_t end = min(it.len1[b], c0 + (uint32_t)kPartChunk);
-        if (tid < kSubs)
-            lcnt[tid] = 0;
-        __syncthreads();
-        const uint32_t* src = a.part1 + it.off1[b];
-        for (uint32_t p = c0 + tid; p < end; p += kPartThreads)
-            atomicAdd(&lcnt[(src[p] >> kSliceBits) & (kSubs - 1)], 1u);
-        __syncthreads();
-        if (tid < kSubs && lcnt[tid])
-            atomicAdd(&cnt2[b * kSubs + tid], lcnt[tid]);
-        __syncthreads();
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const int i = lane * 5 + j;
+        if (i <= kL1Buckets)
+            a.scratch[kOffIstart + i] = run;
+        run += v[j];
     }
 }
 
-// Level 2b: per (bucket, chunk) local sort by slice, runs appended per slice.
-__global__ void __launch_bounds__(kPartThreads) rx_part2_scatter_kernel(HistoArgs a)
+// Level 2: each item = one 16K-key chunk of one bucket's part1 run, sorted
+// by slice ((key >> 14) & 127) in LDS and written back in place as u16
+// slice-local keys, with the run starts of its 128 slices.
+__global__ void __launch_bounds__(kPartThreads) rx_part2_kernel(HistoArgs a)
 {
-    __shared__ L2Items it;
-    __shared__ uint32_t stage[kPartChunk];
-    __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1], soff[kSubs + 1], gpos[kSubs];
-    l2_items_init(a, it);
+    __shared__ uint16_t stage[kPartChunk];
+    __shared__ uint32_t istart[kL1Buckets + 1];
+    __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1];
     const int tid = threadIdx.x;
-    const uint32_t nitems = it.istart[kL1Buckets];
-    const uint32_t* cnt2 = a.scratch + kOffCnt2;
-    uint32_t* cur2 = a.scratch + kOffCur2;
+    for (int b = tid; b <= kL1Buckets; b += kPartThreads)
+        istart[b] = a.scratch[kOffIstart + b];
+    __syncthreads();
+    const uint32_t nitems = istart[kL1Buckets];
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        const int b = find_run(it.istart, kL1Buckets, item);
-        const uint32_t c0 = (item - it.istart[b]) * (uint32_t)kPartChunk;
-        const uint32_t end = min(it.len1[b], c0 + (uint32_t)kPartChunk);
+        const int b = find_run(istart, kL1Buckets, item);
+        const uint32_t c0 = (item - istart[b]) * (uint32_t)kPartChunk;
+        const uint32_t len = a.scratch[kOffCur1 + b];
+        const uint32_t nk = min(len - c0, (uint32_t)kPartChunk);
+        const uint32_t base = a.scratch[kOffOff1 + b] + c0;
         if (tid < kSubs)
             lcnt[tid] = 0;
-        wave0_excl_scan(cnt2 + b * kSubs, soff, kSubs, true);  // slice starts inside the bucket
         __syncthreads();
-        const uint32_t* src = a.part1 + it.off1[b];
         uint32_t key[kPartKeysPerThread], rank[kPartKeysPerThread];
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
-            const uint32_t p = c0 + (uint32_t)(j * kPartThreads + tid);
-            key[j] = p < end ? src[p] : 0u;
-            rank[j] = p < end ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0xffffffffu;
+            const uint32_t p = (uint32_t)(j * kPartThreads + tid);
+            key[j] = p < nk ? a.part1[base + p] : 0u;
+            rank[j] = p < nk ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0xffffffffu;
         }
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kSubs, false);
-        if (tid < kSubs && lcnt[tid])
-            gpos[tid] = it.off1[b] + soff[tid] + atomicAdd(&cur2[b * kSubs + tid], lcnt[tid]);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
             if (rank[j] != 0xffffffffu)
-                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + rank[j]] = key[j];
+                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + rank[j]] =
+                    (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
+        if (tid <= kSubs)
+            a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
         __syncthreads();
-        const uint32_t nkeys = end - c0;
-        for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
-            const uint32_t k = stage[p];
-            const uint32_t sub = (k >> kSliceBits) & (kSubs - 1);
-            a.part2[gpos[sub] + (p - loff[sub])] = k;
-        }
+        for (uint32_t p = tid; p < nk; p += kPartThreads)
+            a.part2[base + p] = stage[p];
         __syncthreads();
     }
 }
 
-// Level 3: one block per 16K-bin slice: LDS histogram of the slice's keys,
-// then one read-modify-write of the slice's table words that received
-// events (16 B per lane, coalesced; untouched 16-B groups are skipped).
+// Level 3: one block per 16K-bin slice: gather the slice's runs from every
+// chunk of its bucket into an LDS histogram, then one read-modify-write of
+// the slice's 64 KB of table (16 B per lane, coalesced, 8 in flight).
 __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
-    __shared__ uint32_t acc[2];
+    __shared__ uint32_t total;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
     const uint32_t s = blockIdx.x;
-    const uint32_t len = a.scratch[kOffCnt2 + s];
-    if (len == 0)
-        return;
     const uint32_t b = s / kSubs, sub = s % kSubs;
-    if (tid < 2)
-        acc[tid] = 0;
-    __syncthreads();
-    // start = off1[b] + sum(cnt2[b*kSubs .. s))
-    uint32_t part = 0;
-    if ((uint32_t)tid < b)
-        part += a.scratch[kOffCnt1 + tid];
-    if (tid >= 300 && (uint32_t)(tid - 300) < sub)
-        part += a.scratch[kOffCnt2 + b * kSubs + (tid - 300)];
-    if (part)
-        atomicAdd(&acc[0], part);
+    const uint32_t i0 = a.scratch[kOffIstart + b], i1 = a.scratch[kOffIstart + b + 1];
+    if (i0 == i1)
+        return;
+    const uint32_t bstart = a.scratch[kOffOff1 + b];
+    if (tid == 0)
+        total = 0;
     u32x4_t* h4 = (u32x4_t*)h;
     for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
-    const uint32_t* src = a.part2 + acc[0];
-    for (uint32_t p = tid; p < len; p += kSliceThreads)
-        atomicAdd(&h[src[p] & ((1u << kSliceBits) - 1)], 1u);
-    __syncthreads();
-    u32x4_t* g4 = (u32x4_t*)(a.hist + ((uint64_t)s << kSliceBits));
-    for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads) {
-        const u32x4_t v = h4[c];
-        if (v.x | v.y | v.z | v.w) {
-            u32x4_t g = g4[c];
-            g += v;  // u32 wrap, like the reference's atomic_fetch_add on u32
-            g4[c] = g;
-        }
+    uint32_t mine = 0;
+    for (uint32_t it = i0 + (uint32_t)wave; it < i1; it += kSliceThreads / 64) {
+        const uint16_t* ro = a.runs + (uint64_t)it * kItemOffs + sub;
+        const uint32_t lo = ro[0], hi = ro[1];
+        const uint16_t* src = a.part2 + bstart + (it - i0) * (uint32_t)kPartChunk;
+        for (uint32_t p = lo + lane; p < hi; p += 64)
+            atomicAdd(&h[src[p]], 1u);
+        mine += hi - lo;
     }
+    if (lane == 0 && mine)
+        atomicAdd(&total, mine);
+    __syncthreads();
+    if (total == 0)
+        return;  // no events for this slice: table untouched
+    u32x4_t* g4 = (u32x4_t*)(a.hist + ((uint64_t)s << kSliceBits));
+    constexpr int kPer = (1 << kSliceBits) / 4 / kSliceThreads;  // 8 x 16 B per thread
+    u32x4_t v[kPer], g[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        g[k] = g4[tid + k * kSliceThreads];
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        v[k] = h4[tid + k * kSliceThreads];
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        g4[tid + k * kSliceThreads] = g[k] + v[k];  // u32 wrap, like the reference's atomic_fetch_add on u32
 }
 
 }  // namespace dqdk
