@@ -722,7 +722,7 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 // Level 1: keys (frame order) -> part1, grouped by bucket = key >> 21.
 // A block stages 16K keys in LDS sorted by bucket, reserves each bucket's
 // run with one global atomic, and writes the runs out contiguously.
-__global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
+__global__ void __launch_bounds__(kPartThreads, 8) rx_part1_kernel(HistoArgs a)  // 2 blocks/CU
 {
     __shared__ uint32_t stage[kPartChunk];
     __shared__ uint32_t off1[kL1Buckets + 1];
@@ -738,7 +738,7 @@ __global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
         for (int b = tid; b < kL1Buckets; b += kPartThreads)
             lcnt[b] = 0;
         __syncthreads();
-        uint32_t key[kPartKeysPerThread], rank[kPartKeysPerThread];
+        uint32_t key[kPartKeysPerThread];
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread / 4; j++) {
             const uint32_t p0 = base + (uint32_t)(j * kPartThreads + tid) * 4;
@@ -756,21 +756,26 @@ __global__ void __launch_bounds__(kPartThreads) rx_part1_kernel(HistoArgs a)
             key[4 * j + 3] = v.w;
 #pragma unroll
             for (int c = 0; c < 4; c++) {
-                const uint32_t k = key[4 * j + c];
-                const bool ok = p0 + c < total && k != DQDK_KEY_NONE;  // non-OK frames hold KEY_NONE
-                rank[4 * j + c] = ok ? atomicAdd(&lcnt[k >> kL1Shift], 1u) : 0xffffffffu;
+                uint32_t& k = key[4 * j + c];
+                if (!(p0 + c < total))
+                    k = DQDK_KEY_NONE;  // non-OK frames already hold KEY_NONE
+                if (k != DQDK_KEY_NONE)
+                    atomicAdd(&lcnt[k >> kL1Shift], 1u);
             }
         }
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kL1Buckets, false);
-        for (int b = tid; b < kL1Buckets; b += kPartThreads)
+        __syncthreads();
+        for (int b = tid; b < kL1Buckets; b += kPartThreads) {
             if (lcnt[b])
                 gpos[b] = off1[b] + atomicAdd(&cur1[b], lcnt[b]);
+            lcnt[b] = loff[b];  // reused as the LDS stage cursor of each bucket
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
-            if (rank[j] != 0xffffffffu)
-                stage[loff[key[j] >> kL1Shift] + rank[j]] = key[j];
+            if (key[j] != DQDK_KEY_NONE)
+                stage[atomicAdd(&lcnt[key[j] >> kL1Shift], 1u)] = key[j];
         __syncthreads();
         const uint32_t nkeys = loff[kL1Buckets];
         for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
@@ -815,7 +820,7 @@ __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 // Level 2: each item = one 16K-key chunk of one bucket's part1 run, sorted
 // by slice ((key >> 14) & 127) in LDS and written back in place as u16
 // slice-local keys, with the run starts of its 128 slices.
-__global__ void __launch_bounds__(kPartThreads) rx_part2_kernel(HistoArgs a)
+__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 2 blocks/CU
 {
     __shared__ uint16_t stage[kPartChunk];
     __shared__ uint32_t istart[kL1Buckets + 1];
@@ -834,23 +839,28 @@ __global__ void __launch_bounds__(kPartThreads) rx_part2_kernel(HistoArgs a)
         if (tid < kSubs)
             lcnt[tid] = 0;
         __syncthreads();
-        uint32_t key[kPartKeysPerThread], rank[kPartKeysPerThread];
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
+        uint32_t key[kPartKeysPerThread];
 #pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++) {
-            const uint32_t p = (uint32_t)(j * kPartThreads + tid);
-            key[j] = p < nk ? a.part1[base + p] : 0u;
-            rank[j] = p < nk ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0xffffffffu;
-        }
+        for (int j = 0; j < kPartKeysPerThread; j++)  // out-of-range lanes read 0 (dropped below)
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)(j * kPartThreads + tid) * 4u, 0, 0);
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            if ((uint32_t)(j * kPartThreads + tid) < nk)
+                atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u);
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kSubs, false);
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)
-            if (rank[j] != 0xffffffffu)
-                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + rank[j]] =
-                    (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
+        if (tid < kSubs)
+            lcnt[tid] = loff[tid];  // reused as the LDS stage cursor of each slice
         if (tid <= kSubs)
             a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            if ((uint32_t)(j * kPartThreads + tid) < nk)
+                stage[atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u)] =
+                    (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         __syncthreads();
         for (uint32_t p = tid; p < nk; p += kPartThreads)
             a.part2[base + p] = stage[p];
@@ -880,12 +890,23 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
     uint32_t mine = 0;
+    constexpr int kG = 4;  // loads in flight per lane
     for (uint32_t it = i0 + (uint32_t)wave; it < i1; it += kSliceThreads / 64) {
         const uint16_t* ro = a.runs + (uint64_t)it * kItemOffs + sub;
         const uint32_t lo = ro[0], hi = ro[1];
         const uint16_t* src = a.part2 + bstart + (it - i0) * (uint32_t)kPartChunk;
-        for (uint32_t p = lo + lane; p < hi; p += 64)
-            atomicAdd(&h[src[p]], 1u);
+        for (uint32_t p0 = lo; p0 < hi; p0 += 64 * kG) {
+            uint32_t k[kG];
+#pragma unroll
+            for (int g = 0; g < kG; g++) {
+                const uint32_t p = p0 + 64 * g + lane;
+                k[g] = p < hi ? (uint32_t)src[p] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int g = 0; g < kG; g++)
+                if (k[g] != 0xffffffffu)
+                    atomicAdd(&h[k[g]], 1u);
+        }
         mine += hi - lo;
     }
     if (lane == 0 && mine)
