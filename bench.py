@@ -104,9 +104,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for i in range(args.steps):
         step()
+        evs[i + 1].record(stream)  # per-step GPU time for the median (no host sync inside)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -126,38 +129,83 @@ def main():
     res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
     assert (res["status"] == D.RX_OK).all(), np.bincount(res["status"])
 
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    step_median_ms = step_ms[len(step_ms) // 2]
     total_pkts = n * args.steps * world
     mpkts = total_pkts / elapsed / 1e6
     frame_gbs = total_pkts * L / elapsed / 1e9
 
-    # ---- roofline of the dominant kernel (HIP events on the queue stream) ----
+    # ---- per-kernel algorithmic bytes per launch ------------
+    K = n * E  # decoded records per batch
+    items = K // (1 << 14) + 284 + 1  # part2 work items (16K-key chunks of the 284 buckets)
+    runs = items * 129 * 2  # u16 slice-run offsets per item
+    touched = 0
+    if histo and E:
+        kk = d_keys[:K]
+        touched = int(torch.unique(kk[kk >= 0] >> 14).numel())  # 16K-bin slices with >= 1 event
     alg = {
-        # per-frame algorithmic bytes: desc + frame + result (+ 4-B record per event)
-        "rx_decode": 16 + L + 8 + 4 * E,
-        # keys read + one u32 read-modify-write per event, plus the 8-B result read
-        "histogram": 8 + 12 * E,
-        "counters": 2 * 8,
+        # the metric's path: desc + frame (the UDP checksum reads all of it) + result + 4-B record per event
+        "rx_decode": n * (16 + L + 8) + 4 * K,
+        "rx_abort": 8 * n,
+        "rx_count": 8 * n,
+        "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
+        "rx_part1": 8 * n + 8 * K,
+        "rx_hist_prep": 0,
+        "rx_part2": 6 * K + runs,
+        # u16 keys + runs read, one read-modify-write sweep of every touched 64 KB slice
+        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 16),
     }
     st = {}
     for name, s in stages.items():
         if s["launches"]:
             avg_ms = s["ms"] / s["launches"]
-            gbs = alg[name] * n / (avg_ms * 1e-3) / 1e9
-            st[name] = {"avg_ms": round(avg_ms, 4), "alg_bytes_per_frame": alg[name], "GB_s": round(gbs, 1),
-                        "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
-    if "histogram" in st:
-        st["histogram"]["Gupdates_s"] = round(n * E / (st["histogram"]["avg_ms"] * 1e-3) / 1e9, 2)
+            gbs = alg[name] / (avg_ms * 1e-3) / 1e9
+            st[name] = {"avg_ms": round(avg_ms, 4), "launches": s["launches"], "alg_bytes": alg[name],
+                        "GB_s": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+
+    # measured bounds on this GPU (membench.hip): streaming read over the UMEM
+    # image, random u32 atomics of the same records into a scratch table
+    import ctypes as C
+
+    from dqdk_amd import _lib as LIB
+    ms = C.c_double()
+    LIB.check(LIB.lib().dqdk_gpu_membench_read(d_umem.data_ptr(), umem_bytes // 16 * 16, stream.cuda_stream, 5,
+                                               C.byref(ms)), "membench_read")
+    stream_gbs = umem_bytes // 16 * 16 / (ms.value * 1e-3) / 1e9
+
+    hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo") if k in st]
+    histogram = None
+    if hist_kernels:
+        h_ms = sum(st[k]["avg_ms"] for k in hist_kernels)
+        scratch = torch.zeros(D.HISTO_ENTRIES, dtype=torch.int32, device=dev)
+        LIB.check(LIB.lib().dqdk_gpu_membench_atomic(scratch.data_ptr(), D.HISTO_ENTRIES, d_keys.data_ptr(), K,
+                                                     stream.cuda_stream, 3, C.byref(ms)), "membench_atomic")
+        del scratch
+        atomic_gupd = K / (ms.value * 1e-3) / 1e9
+        gupd = K / (h_ms * 1e-3) / 1e9
+        histogram = {"kernels": hist_kernels, "updates_per_batch": K, "touched_slices": touched,
+                     "ms": round(h_ms, 4), "Gupd_s": round(gupd, 2),
+                     "bound": {"kind": "random u32 atomic increment, measured on these records "
+                                       "(dqdk_gpu_membench_atomic)", "Gupd_s": round(atomic_gupd, 2)},
+                     "vs_bound": round(gupd / atomic_gupd, 3)}
+
+    # ---- roofline: rx_decode, the kernel §8(d)'s per-packet bytes price -----
     dom = max(st, key=lambda k: st[k]["avg_ms"]) if st else "rx_decode"
     traffic = None
     try:
         pmc = json.loads(Path(args.pmc).read_text())
         w = pmc.get(f"{L}:{'csum' if not args.no_csum else 'nocsum'}:{n}", {})
-        traffic = w.get(dom, {}).get("hbm_bytes_per_launch")
+        traffic = w.get("rx_decode", {}).get("hbm_bytes_per_launch")
     except Exception:
         pass
-    roofline = {"bound": "hbm", "kernel": dom,
-                "achieved": st.get(dom, {}).get("GB_s"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": st.get(dom, {}).get("frac_hbm"), "traffic": traffic}
+    dec = st.get("rx_decode", {})
+    roofline = {"bound": "hbm", "kernel": "rx_decode",
+                "achieved": dec.get("GB_s"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dec.get("frac_hbm"), "traffic": traffic,
+                "alg_bytes_per_frame": 16 + L + 8 + 4 * E, "frames_per_launch": n,
+                "measured_stream_read_GB_s": round(stream_gbs, 1),
+                "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
+                "slowest_kernel": dom}
 
     # ---- CPU baseline: the oracle (C restatement) on rank 0 at N=1 ----------
     cpu = None
@@ -185,7 +233,10 @@ def main():
                        "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
                        "parallelism": f"queue-per-gpu x{world}"},
             "frame_GB_s": round(frame_gbs, 2),
-            "stages": st,
+            "step_ms_median": round(step_median_ms, 4),
+            "step_ms_min": round(step_ms[0], 4),
+            "kernels": st,
+            "histogram": histogram,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -213,10 +264,23 @@ def cpu_baseline(umem, desc, cfg, histo, budget_sec):
         sec += s
         passes += 1
     rate = sample * passes / sec / 1e6
+    # one pinned worker per queue is the reference's model (src/dqdk.c:517-620):
+    # 2/4/8 workers on 2/4/8 x the sample, sharing the table (relaxed atomics)
+    threads = {}
+    for t in (2, 4, 8):
+        m = min(len(desc), t * sample)
+        st, _ = O.rx_batch_threads(umem, desc[:m], cfg.payloadsz, cfg.mode, cfg.flags, hist, threads=t)
+        threads[str(t)] = round(m / st / 1e6, 4)
+    model = ""
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        pass
     return {"value": round(rate, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} frames of the workload x {passes} passes ({sec:.1f} s), "
-                      f"1 thread, histogram {'on (2.38 GB table)' if histo else 'off'}, "
-                      f"host {_os.cpu_count()} cpus"}
+                      f"1 thread, histogram {'on (2.38 GB table)' if histo else 'off'}; "
+                      f"host {model}, nproc {_os.cpu_count()}",
+            "threads_Mpkt_s": threads}
 
 
 if __name__ == "__main__":

@@ -66,6 +66,7 @@ MODES = {"waveform": MODE_WAVEFORM, "listwave": MODE_LISTWAVE, "listmode": MODE_
 F_CSUM, F_BATCH_ABORT, F_PREFILTER, F_NO_HISTO, F_CSUM_WRITEBACK = 1, 2, 4, 8, 16
 F_HISTO_ATOMIC, F_HISTO_PARTITIONED = 32, 64
 KEY_NONE = 0xFFFFFFFF
+TIMING_STAGES = 8
 HISTO_CHANNELS, HISTO_HISTS, HISTO_BINS = 1512, 6, 65536
 HISTO_ENTRIES = HISTO_CHANNELS * HISTO_HISTS * HISTO_BINS
 
@@ -90,8 +91,17 @@ SIGNATURES = {
     "dqdk_gpu_histogram_accumulate": (C.c_int, [_P, _P]),
     "dqdk_gpu_histogram_reset": (C.c_int, [_P]),
     "dqdk_gpu_histogram_device_ptr": (_P, [_P]),
+    "dqdk_gpu_histogram_copy": (C.c_int, [_P, _P]),
+    "dqdk_gpu_histogram_add": (C.c_int, [_P, _P]),
+    "dqdk_gpu_histogram_nonzero": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "dqdk_gpu_histogram_write_csv": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
+    "dqdk_gpu_tristan_summary": (C.c_int, [C.POINTER(C.POINTER(Counters)), C.c_int, C.POINTER(C.c_uint64),
+                                           C.c_char_p, C.c_char_p, C.c_uint64]),
+    "dqdk_gpu_membench_read": (C.c_int, [_P, C.c_uint64, _P, C.c_int, C.POINTER(C.c_double)]),
+    "dqdk_gpu_membench_atomic": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, _P, C.c_int, C.POINTER(C.c_double)]),
     "dqdk_gpu_timing_enable": (C.c_int, [_P, C.c_int]),
     "dqdk_gpu_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
+    "dqdk_gpu_timing_stage_name": (C.c_char_p, [C.c_int]),
     "dqdk_gpu_last_error": (C.c_char_p, []),
     "dqdk_synth_umem_size": (C.c_uint64, [C.POINTER(SynthCfg), C.c_uint32]),
     "dqdk_synth_frame_len": (C.c_uint32, [C.POINTER(SynthCfg), C.c_uint64]),

@@ -11,11 +11,13 @@
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "egress_kernels.h"
 #include "rx_kernels.h"
 
 using namespace dqdk;
@@ -43,7 +45,10 @@ int fail_errno(int err, const char* what)
             return fail(#x, e_);            \
     } while (0)
 
-constexpr int kStages = 3;
+constexpr int kStages = DQDK_GPU_TIMING_STAGES;
+enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice };
+const char* const kStageNames[kStages] = {"rx_decode", "rx_abort",     "rx_count", "rx_histo_atomic",
+                                          "rx_part1",  "rx_hist_prep", "rx_part2", "rx_slice_histo"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
@@ -97,8 +102,8 @@ struct dqdk_gpu_queue {
         hipEvent_t a, b;
     };
     std::vector<Pending> pending;
-    double stage_ms[kStages] = {0, 0, 0};
-    uint64_t counts[kStages] = {0, 0, 0};
+    double stage_ms[kStages] = {};
+    uint64_t counts[kStages] = {};
 };
 
 namespace {
@@ -171,10 +176,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t grid_dec = std::min<uint32_t>(ntiles, (uint32_t)q->cu_count * 8u);
     {
-        StageTimer t(q, 0);
+        StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_decode_kernel, dim3(grid_dec), dim3(kTile), 0, q->stream, ra);
-        HIPCHK(hipGetLastError());
     }
+    HIPCHK(hipGetLastError());
 
     CountArgs ca{};
     ca.res = d_res;
@@ -186,11 +191,14 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ca.cum = q->d_cum;
     const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
     {
-        StageTimer t(q, 1);
+        StageTimer t(q, kStAbort);
         hipLaunchKernelGGL(rx_abort_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
-        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
-        HIPCHK(hipGetLastError());
     }
+    {
+        StageTimer t(q, kStCount);
+        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
+    }
+    HIPCHK(hipGetLastError());
 
     if (q->histo && q->E) {
         HistoArgs ha{};
@@ -205,19 +213,31 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.part1 = q->d_part1;
         ha.part2 = q->d_part2;
         ha.runs = q->d_runs;
-        StageTimer t(q, 2);
         if (!partitioned) {
             const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
+            StageTimer t(q, kStAtomic);
             hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
         } else {
             const uint64_t nkeys = (uint64_t)n * q->E;
             const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
             const uint32_t grid_p = std::min<uint32_t>(chunks, (uint32_t)q->cu_count * 2u);
             const uint32_t grid_l2 = std::min<uint32_t>(chunks + kL1Buckets, (uint32_t)q->cu_count * 2u);
-            hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kPartThreads), 0, q->stream, ha);
-            hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(64), 0, q->stream, ha);
-            hipLaunchKernelGGL(rx_part2_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
-            hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+            {
+                StageTimer t(q, kStPart1);
+                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kPartThreads), 0, q->stream, ha);
+            }
+            {
+                StageTimer t(q, kStPrep);
+                hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(64), 0, q->stream, ha);
+            }
+            {
+                StageTimer t(q, kStPart2);
+                hipLaunchKernelGGL(rx_part2_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+            }
+            {
+                StageTimer t(q, kStSlice);
+                hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+            }
         }
         HIPCHK(hipGetLastError());
     }
@@ -545,5 +565,192 @@ int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts
     }
     return 0;
 }
+
+int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst)
+{
+    if (!q || !d_dst)
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_copy: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    HIPCHK(hipMemcpyAsync(d_dst, q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          q->stream));
+    return 0;
+}
+
+int dqdk_gpu_histogram_add(dqdk_gpu_queue_t* q, const uint32_t* d_src)
+{
+    if (!q || !d_src || ((uintptr_t)d_src & 15))
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_add: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    const uint64_t n16 = DQDK_TRISTAN_HISTO_ENTRIES / 4;
+    hipLaunchKernelGGL(hist_add_kernel, dim3((uint32_t)q->cu_count * 8u), dim3(256), 0, q->stream, q->d_hist, d_src, n16);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int dqdk_gpu_histogram_nonzero(dqdk_gpu_queue_t* q, uint64_t* count)
+{
+    if (!q || !count)
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_nonzero: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(*d)));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), q->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(hist_nonzero_kernel, dim3((uint32_t)q->cu_count * 8u), dim3(256), 0, q->stream, q->d_hist,
+                           DQDK_TRISTAN_HISTO_ENTRIES / 4, d);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, q->stream);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(q->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess)
+        return fail("histogram_nonzero", e);
+    *count = h;
+    return 0;
+}
+
+namespace {
+
+int write_all(int fd, const char* p, uint64_t n)
+{
+    while (n) {
+        const ssize_t w = write(fd, p, n > (1u << 30) ? (1u << 30) : (size_t)n);
+        if (w < 0) {
+            if (errno == EINTR)
+                continue;
+            const int err = errno;
+            g_err = std::string("histogram_write_csv: write: ") + strerror(err);
+            return -err;
+        }
+        p += w;
+        n -= (uint64_t)w;
+    }
+    return 0;
+}
+
+}  // namespace
+
+int dqdk_gpu_histogram_write_csv(dqdk_gpu_queue_t* q, int fd, uint64_t* bytes_written)
+{
+    if (!q || fd < 0)
+        return -EINVAL;
+    if (!q->d_hist)
+        return fail_errno(-ENOENT, "histogram_write_csv: queue has no histogram");
+    HIPCHK(hipSetDevice(q->device));
+    static const char header[] = "Channel,Histo,Energy,Freq\n";  // src/tristan.c:198
+    int rc = write_all(fd, header, sizeof(header) - 1);
+    if (rc)
+        return rc;
+    uint64_t total = sizeof(header) - 1;
+
+    // Two text buffers: the GPU formats chunk c+1 while the host writes chunk c.
+    const uint64_t cap = kCsvChunkBins * kCsvMaxLine;
+    uint64_t* d_blk[2] = {nullptr, nullptr};
+    char* d_txt[2] = {nullptr, nullptr};
+    char* h_txt[2] = {nullptr, nullptr};
+    uint64_t* h_len = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < 2 && e == hipSuccess; b++) {
+        e = hipMalloc(&d_blk[b], (kCsvChunkBlocks + 1) * sizeof(uint64_t));
+        if (e == hipSuccess)
+            e = hipMalloc(&d_txt[b], cap);
+        if (e == hipSuccess)
+            e = hipHostMalloc(&h_txt[b], cap, hipHostMallocDefault);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
+    }
+    if (e == hipSuccess)
+        e = hipHostMalloc(&h_len, 2 * sizeof(uint64_t), hipHostMallocDefault);
+
+    const uint64_t N = DQDK_TRISTAN_HISTO_ENTRIES;
+    const uint64_t nchunks = (N + kCsvChunkBins - 1) / kCsvChunkBins;
+    // Enqueue chunk c into buffer b: format on the GPU, copy the text back.
+    // The text length is needed before the copy, so each chunk's length is
+    // read back with a small copy and the text copy is sized on the host.
+    auto format = [&](uint64_t c, int b) -> hipError_t {
+        const uint64_t base = c * kCsvChunkBins, end = std::min(N, base + kCsvChunkBins);
+        const uint32_t nblk = (uint32_t)((end - base + kCsvBinsPerBlock - 1) / kCsvBinsPerBlock);
+        hipLaunchKernelGGL(csv_len_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, base, end, d_blk[b]);
+        hipLaunchKernelGGL(csv_scan_kernel, dim3(1), dim3(1024), 0, q->stream, d_blk[b], nblk);
+        hipLaunchKernelGGL(csv_write_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, base, end, d_blk[b],
+                           d_txt[b]);
+        hipError_t r = hipGetLastError();
+        if (r == hipSuccess)
+            r = hipMemcpyAsync(&h_len[b], d_blk[b] + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost, q->stream);
+        if (r == hipSuccess)
+            r = hipStreamSynchronize(q->stream);
+        if (r == hipSuccess && h_len[b])
+            r = hipMemcpyAsync(h_txt[b], d_txt[b], h_len[b], hipMemcpyDeviceToHost, q->stream);
+        if (r == hipSuccess)
+            r = hipEventRecord(done[b], q->stream);
+        return r;
+    };
+    if (e == hipSuccess && nchunks)
+        e = format(0, 0);
+    for (uint64_t c = 0; e == hipSuccess && rc == 0 && c < nchunks; c++) {
+        const int b = (int)(c & 1);
+        e = hipEventSynchronize(done[b]);
+        const uint64_t len = h_len[b];
+        if (e == hipSuccess && c + 1 < nchunks)
+            e = format(c + 1, b ^ 1);  // formats while this thread writes chunk c
+        if (e == hipSuccess && len) {
+            rc = write_all(fd, h_txt[b], len);
+            total += len;
+        }
+    }
+    (void)hipStreamSynchronize(q->stream);
+    for (int b = 0; b < 2; b++) {
+        (void)hipFree(d_blk[b]);
+        (void)hipFree(d_txt[b]);
+        (void)hipHostFree(h_txt[b]);
+        if (done[b])
+            (void)hipEventDestroy(done[b]);
+    }
+    (void)hipHostFree(h_len);
+    if (e != hipSuccess)
+        return fail("histogram_write_csv", e);
+    if (rc)
+        return rc;
+    if (bytes_written)
+        *bytes_written = total;
+    return 0;
+}
+
+int dqdk_gpu_tristan_summary(const dqdk_gpu_counters_t* const* per_queue, int nqueues, const uint64_t* runtime_ns,
+                             const char* directory, char* buf, uint64_t bufsz)
+{
+    if (!per_queue || nqueues < 0 || !buf || !bufsz)
+        return -EINVAL;
+    unsigned long long ev = 0, by = 0, pk = 0;
+    uint64_t rt = 0;
+    for (int k = 0; k < nqueues; k++) {
+        if (!per_queue[k])
+            return -EINVAL;
+        ev += per_queue[k]->total_events;  // tristan_t atomics (src/tristan.c:172-175)
+        by += per_queue[k]->total_bytes;
+        pk += per_queue[k]->rcvd_pkts;     // sum of worker rcvd_pkts (:177-183)
+        if (runtime_ns && runtime_ns[k] > rt)
+            rt = runtime_ns[k];            // max worker runtime
+    }
+    const int n = snprintf(buf, bufsz,
+                           "{ \"total_received_events\": %llu,\"total_received_bytes\": %llu, "
+                           "\"total_received_packets\": %llu, \"dqdk_runtime_ms\": %.2lf, \"directory\": \"%s\"}",
+                           ev, by, pk, (double)rt / 1e6, directory ? directory : "(null)");
+    if (n < 0)
+        return -EINVAL;
+    return n;  // like snprintf: characters the full string needs
+}
+
+const char* dqdk_gpu_timing_stage_name(int stage) { return stage >= 0 && stage < kStages ? kStageNames[stage] : nullptr; }
 
 }  // extern "C"

@@ -1,0 +1,204 @@
+/*
+ * egress_kernels.hip -- histogram egress on the GPU.
+ *
+ * tristan_fini (src/tristan.c:197-216) walks the 2.38 GB table on the host
+ * and dprintf()s "%d,%d,%u,%u\n" = channel, histogram, energy bin, count for
+ * every non-zero bin in table order.  Here the table never leaves HBM: for
+ * each chunk of bins the GPU
+ *   csv_len     -- counts the characters of every line a 4096-bin block
+ *                  will emit (one 64-B row of 16 bins per thread),
+ *   csv_scan    -- exclusive-scans the block totals (one block),
+ *   csv_write   -- re-reads its bins, block-scans the per-thread lengths
+ *                  and writes the formatted lines at their final offsets,
+ * so only the CSV text crosses PCIe.  Plus the end-of-run merge helpers
+ * (u32-wrapping add of another table, non-zero count).
+ */
+#include "egress_kernels.h"
+
+namespace dqdk {
+
+namespace {
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-B streaming load (nontemporal: the bytes are used once)
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p)
+{
+    const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t ndigits(uint32_t v)
+{
+    return 1u + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
+           (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
+}
+
+// "%d,%d,%u,%u\n" of flat bin k = (channel*6 + histogram)*65536 + energy
+__device__ __forceinline__ uint32_t line_len(uint64_t k, uint32_t freq)
+{
+    const uint32_t ch = (uint32_t)(k / (6u * 65536u));
+    const uint32_t e = (uint32_t)(k & 0xFFFFu);
+    return ndigits(ch) + 1u + 1u + 1u + ndigits(e) + 1u + ndigits(freq) + 1u;
+}
+
+__device__ __forceinline__ char* put_u32(char* p, uint32_t v)
+{
+    const uint32_t n = ndigits(v);
+    for (uint32_t d = n; d-- > 0;) {
+        p[d] = (char)('0' + v % 10u);
+        v /= 10u;
+    }
+    return p + n;
+}
+
+__device__ __forceinline__ void load_row(const uint32_t* hist, uint64_t first, uint64_t end, uint32_t v[kCsvBinsPerThread])
+{
+    if (first + kCsvBinsPerThread <= end) {
+        const uint4* p = (const uint4*)(hist + first);
+#pragma unroll
+        for (int j = 0; j < kCsvBinsPerThread / 4; j++) {
+            const uint4 x = ld_nt16(p + j);
+            v[4 * j] = x.x;
+            v[4 * j + 1] = x.y;
+            v[4 * j + 2] = x.z;
+            v[4 * j + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kCsvBinsPerThread; j++)
+            v[j] = first + j < end ? hist[first + j] : 0u;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T* lds_wave, T* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T t = __shfl_up(incl, o);
+        if (lane >= o)
+            incl += t;
+    }
+    if (lane == 63)
+        lds_wave[w] = incl;
+    __syncthreads();
+    T base = 0, all = 0;
+    for (int j = 0; j < (int)(blockDim.x >> 6); j++) {
+        if (j < w)
+            base += lds_wave[j];
+        all += lds_wave[j];
+    }
+    *total = all;
+    return base + incl - x;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kCsvThreads) void csv_len_kernel(const uint32_t* __restrict__ hist, uint64_t base, uint64_t end,
+                                                             uint64_t* __restrict__ blk_chars)
+{
+    __shared__ uint64_t lds[kCsvThreads / 64];
+    const uint64_t first = base + ((uint64_t)blockIdx.x * kCsvThreads + threadIdx.x) * kCsvBinsPerThread;
+    uint32_t v[kCsvBinsPerThread];
+    uint64_t chars = 0;
+    if (first < end) {
+        load_row(hist, first, end, v);
+#pragma unroll
+        for (int j = 0; j < kCsvBinsPerThread; j++)
+            chars += v[j] ? line_len(first + j, v[j]) : 0u;
+    }
+    uint64_t total;
+    (void)block_excl_scan<uint64_t>(chars, lds, &total);
+    if (threadIdx.x == 0)
+        blk_chars[blockIdx.x] = total;
+}
+
+// One block: in-place exclusive scan of nblk u64 block totals; [nblk] = grand total.
+__global__ __launch_bounds__(1024) void csv_scan_kernel(uint64_t* __restrict__ blk_chars, uint32_t nblk)
+{
+    __shared__ uint64_t lds[16];
+    uint64_t carry = 0;
+    for (uint32_t c = 0; c < nblk; c += blockDim.x) {
+        const uint32_t i = c + threadIdx.x;
+        const uint64_t x = i < nblk ? blk_chars[i] : 0u;
+        uint64_t total;
+        const uint64_t ex = block_excl_scan<uint64_t>(x, lds, &total);
+        if (i < nblk)
+            blk_chars[i] = carry + ex;
+        carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        blk_chars[nblk] = carry;
+}
+
+__global__ __launch_bounds__(kCsvThreads) void csv_write_kernel(const uint32_t* __restrict__ hist, uint64_t base, uint64_t end,
+                                                               const uint64_t* __restrict__ blk_off, char* __restrict__ out)
+{
+    __shared__ uint64_t lds[kCsvThreads / 64];
+    const uint64_t first = base + ((uint64_t)blockIdx.x * kCsvThreads + threadIdx.x) * kCsvBinsPerThread;
+    uint32_t v[kCsvBinsPerThread];
+    uint64_t chars = 0;
+    if (first < end) {
+        load_row(hist, first, end, v);
+#pragma unroll
+        for (int j = 0; j < kCsvBinsPerThread; j++)
+            chars += v[j] ? line_len(first + j, v[j]) : 0u;
+    }
+    uint64_t total;
+    const uint64_t off = blk_off[blockIdx.x] + block_excl_scan<uint64_t>(chars, lds, &total);
+    if (!chars)
+        return;
+    char* p = out + off;
+#pragma unroll 1
+    for (int j = 0; j < kCsvBinsPerThread; j++) {
+        if (!v[j])
+            continue;
+        const uint64_t k = first + j;
+        const uint32_t ch = (uint32_t)(k / (6u * 65536u));
+        const uint32_t h = (uint32_t)((k >> 16) % 6u);
+        p = put_u32(p, ch);
+        *p++ = ',';
+        *p++ = (char)('0' + h);
+        *p++ = ',';
+        p = put_u32(p, (uint32_t)(k & 0xFFFFu));
+        *p++ = ',';
+        p = put_u32(p, v[j]);
+        *p++ = '\n';
+    }
+}
+
+__global__ __launch_bounds__(256) void hist_add_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t n16)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        uint4 a = ((const uint4*)dst)[i];
+        const uint4 b = ld_nt16((const uint4*)src + i);
+        a.x += b.x;  // u32 wrap, like the shared relaxed-atomic table
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+        ((uint4*)dst)[i] = a;
+    }
+}
+
+__global__ __launch_bounds__(256) void hist_nonzero_kernel(const uint32_t* __restrict__ hist, uint64_t n16,
+                                                          unsigned long long* __restrict__ count)
+{
+    __shared__ uint32_t lds[4];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint4 a = ld_nt16((const uint4*)hist + i);
+        c += (a.x != 0) + (a.y != 0) + (a.z != 0) + (a.w != 0);
+    }
+    uint32_t total;
+    (void)block_excl_scan<uint32_t>(c, lds, &total);
+    if (threadIdx.x == 0 && total)
+        atomicAdd(count, (unsigned long long)total);
+}
+
+}  // namespace dqdk

@@ -83,12 +83,22 @@ __device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uin
 }
 
 // bytes at rel. offset [lo, hi) of a dword starting at rel. offset p -> mask
-__device__ __forceinline__ uint32_t range_mask(int p, int lo, int hi)
+// Sums of the even- and odd-position bytes [from, to) (0 <= from <= to <= 16)
+// of one 16-B chunk held in wave-uniform registers (scalar ALU).
+__device__ __forceinline__ void chunk_range_sums(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, int from, int to,
+                                                 uint32_t& e, uint32_t& o)
 {
-    int a = lo - p, b = hi - p;
-    uint32_t ml = a <= 0 ? 0xffffffffu : (a >= 4 ? 0u : (0xffffffffu << (8 * a)));
-    uint32_t mh = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : (0xffffffffu >> (32 - 8 * b)));
-    return ml & mh;
+    auto below = [](int nbytes) -> uint64_t {
+        return nbytes <= 0 ? 0ull : nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1);
+    };
+    const uint64_t lo = ((uint64_t)x0 | ((uint64_t)x1 << 32)) & (below(to) & ~below(from));
+    const uint64_t hi = ((uint64_t)x2 | ((uint64_t)x3 << 32)) & (below(to - 8) & ~below(from - 8));
+    const uint64_t M = 0x00ff00ff00ff00ffull;
+    uint64_t se = (lo & M) + (hi & M), so = ((lo >> 8) & M) + ((hi >> 8) & M);
+    se += se >> 32;
+    so += so >> 32;
+    e = (uint32_t)(se & 0xffffu) + (uint32_t)((se >> 16) & 0xffffu);
+    o = (uint32_t)(so & 0xffffu) + (uint32_t)((so >> 16) & 0xffffu);
 }
 
 
@@ -343,7 +353,8 @@ __device__ __forceinline__ void wave_frame(const RxArgs& a, const LaneFrame& lf,
 __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame& P, uint32_t slot, int w,
                                                const u32x4& v, int lane, bool active,
                                                __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc_e,
-                                               uint32_t& acc_o, uint32_t& oob, uint32_t* lds_cnt1)
+                                               uint32_t& acc_o, uint32_t& corr_e, uint32_t& corr_o, uint32_t& oob,
+                                               uint32_t* lds_cnt1)
 {
     const int c0 = P.c_begin + 64 * w;
     const int c = c0 + lane;
@@ -355,22 +366,32 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
         const bool incs = inr && c <= P.ct;
         te = incs ? te : 0u;
         to = incs ? to : 0u;
-        if (active && (w == 0 || (P.ct >= c0 && P.ct < c0 + 64))) {
-            // uniform: this window holds the first or the last checksum chunk;
-            // drop their bytes outside [cs_lo, cs_hi) (cs_hi includes the
-            // odd-length over-read byte)
-            const int p = 16 * c + P.q4;
-            uint32_t de = 0, dd = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t wk = (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) &
-                                    ~range_mask(p + 4 * k, P.cs_lo, P.cs_hi);
-                de += wk & M;
-                dd += (wk >> 8) & M;
+        if (active) {
+            // uniform: the first checksum chunk (lane 0 of window 0) and the
+            // last one (chunk ct) may hold bytes outside [cs_lo, cs_hi)
+            // (cs_hi includes the odd-length over-read byte); their sums are
+            // taken from the owning lane's data in SGPRs and subtracted from
+            // the frame total at its end
+            if (w == 0) {
+                const int nb = P.cs_lo - (16 * P.c_begin + P.q4);
+                if (nb > 0) {
+                    uint32_t de, dd;
+                    chunk_range_sums(rdl(v.x, 0), rdl(v.y, 0), rdl(v.z, 0), rdl(v.w, 0), 0, nb, de, dd);
+                    corr_e += de;
+                    corr_o += dd;
+                }
             }
-            const bool edge = incs && (c == P.c_begin || c == P.ct);
-            te -= edge ? de : 0u;
-            to -= edge ? dd : 0u;
+            const int lt = P.ct - c0;
+            if (lt >= 0 && lt < 64) {
+                const int keep = P.cs_hi - (16 * P.ct + P.q4);
+                if (keep < 16) {
+                    const uint32_t l = (uint32_t)lt;
+                    uint32_t de, dd;
+                    chunk_range_sums(rdl(v.x, l), rdl(v.y, l), rdl(v.z, l), rdl(v.w, l), keep, 16, de, dd);
+                    corr_e += de;
+                    corr_o += dd;
+                }
+            }
         }
         acc_e += (te & 0xffff) + (te >> 16);
         acc_o += (to & 0xffff) + (to >> 16);
@@ -454,17 +475,18 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
         int wp = 0;
         WaveFrame P;
         wave_frame(a, lf, jp, false, P);
-        uint32_t acc_e = 0, acc_o = 0, oob = 0;
+        uint32_t acc_e = 0, acc_o = 0, oob = 0, corr_e = 0, corr_o = 0;
         for (int k = 0; k < total; k += kRing) {
 #pragma unroll
             for (int d = 0; d < kRing; d++) {
                 const bool active = k + d < total;
-                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, oob, lds_cnt1);
+                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, corr_e, corr_o, oob,
+                               lds_cnt1);
                 if (active && ++wp == P.nwin) {
                     // hand the frame's totals to its owning lane
                     const bool owner = lane == (int)jp;
                     if (P.work & 2) {
-                        const uint32_t se = wave_sum_dpp(acc_e), so = wave_sum_dpp(acc_o);
+                        const uint32_t se = wave_sum_dpp(acc_e) - corr_e, so = wave_sum_dpp(acc_o) - corr_o;
                         sum_e = owner ? se : sum_e;
                         sum_o = owner ? so : sum_o;
                     }
@@ -472,7 +494,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
                         const uint32_t so = wave_sum_dpp(oob);
                         sum_oob = owner ? so : sum_oob;
                     }
-                    acc_e = acc_o = oob = 0;
+                    acc_e = acc_o = oob = corr_e = corr_o = 0;
                     wp = 0;
                     pmask &= pmask - 1;
                     if (pmask) {

@@ -160,16 +160,47 @@ class RxQueue:
     def histogram_device_ptr(self) -> int | None:
         return L.lib().dqdk_gpu_histogram_device_ptr(self._h)
 
+    def histogram_copy(self, d_dst_ptr: int) -> None:
+        """Async device copy of the table into a caller buffer (e.g. an RCCL reduce buffer)."""
+        L.check(L.lib().dqdk_gpu_histogram_copy(self._h, d_dst_ptr), "histogram_copy")
+
+    def histogram_add(self, d_src_ptr: int) -> None:
+        """Async table += caller device buffer (u32 wrap): the cross-queue merge."""
+        L.check(L.lib().dqdk_gpu_histogram_add(self._h, d_src_ptr), "histogram_add")
+
+    def histogram_nonzero(self) -> int:
+        c = C.c_uint64()
+        L.check(L.lib().dqdk_gpu_histogram_nonzero(self._h, C.byref(c)), "histogram_nonzero")
+        return int(c.value)
+
+    def write_histogram_csv(self, fd: int) -> int:
+        """The histogram file of tristan_fini (src/tristan.c:197-216), formatted on the GPU."""
+        n = C.c_uint64()
+        L.check(L.lib().dqdk_gpu_histogram_write_csv(self._h, fd, C.byref(n)), "histogram_write_csv")
+        return int(n.value)
+
     # -- stage timing --------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:
         L.check(L.lib().dqdk_gpu_timing_enable(self._h, int(on)), "timing_enable")
 
     def read_timing(self) -> dict:
-        ms = (C.c_double * 3)()
-        cnt = (C.c_uint64 * 3)()
-        L.check(L.lib().dqdk_gpu_timing_read(self._h, ms, cnt, 3), "timing_read")
-        names = ("rx_decode", "counters", "histogram")
-        return {names[k]: {"ms": ms[k], "launches": int(cnt[k])} for k in range(3)}
+        """Per-kernel HIP-event totals since the last read: {kernel: {ms, launches}}."""
+        ns = L.TIMING_STAGES
+        ms = (C.c_double * ns)()
+        cnt = (C.c_uint64 * ns)()
+        L.check(L.lib().dqdk_gpu_timing_read(self._h, ms, cnt, ns), "timing_read")
+        return {L.lib().dqdk_gpu_timing_stage_name(k).decode(): {"ms": ms[k], "launches": int(cnt[k])}
+                for k in range(ns)}
+
+
+def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, directory: str = "") -> str:
+    """tristan_fini's controller status line (src/tristan.c:171-189) via the C ABI."""
+    objs = [L.Counters(**{f: int(c.get(f, 0)) for f in L.COUNTER_FIELDS}) for c in counters]
+    arr = (C.POINTER(L.Counters) * max(len(objs), 1))(*[C.pointer(o) for o in objs])
+    rt = (C.c_uint64 * max(len(objs), 1))(*(runtime_ns or [0] * len(objs)))
+    buf = C.create_string_buffer(8192)  # buffersz in tristan_fini
+    L.check(L.lib().dqdk_gpu_tristan_summary(arr, len(objs), rt, directory.encode(), buf, 8192), "tristan_summary")
+    return buf.value.decode()
 
 
 # ---- synthetic UMEM (bench / test input) ------------------------------------

@@ -168,12 +168,48 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
 /* Device pointer of the histogram (for RCCL reduce across GPUs), or NULL. */
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
 
+/* ---- end-of-run egress (tristan_fini, src/tristan.c:162-233) ------------- */
+/* Merge helpers for per-GPU partial tables.  d_dst / d_src are device
+ * pointers to DQDK_TRISTAN_HISTO_ENTRIES u32 (16-B aligned) reachable from
+ * the queue's device; both run async on the queue stream.  copy: d_dst =
+ * table (e.g. into an RCCL reduce buffer); add: table += d_src (u32 wrap). */
+int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst);
+int dqdk_gpu_histogram_add(dqdk_gpu_queue_t* q, const uint32_t* d_src);
+/* Number of non-zero bins (synchronous). */
+int dqdk_gpu_histogram_nonzero(dqdk_gpu_queue_t* q, uint64_t* count);
+/* Write the histogram file of tristan_fini (src/tristan.c:197-216) to fd:
+ * the header "Channel,Histo,Energy,Freq\n" then "%d,%d,%u,%u\n" (channel,
+ * histogram, energy bin, count) for every non-zero bin in table order.  The
+ * text is formatted on the GPU chunk by chunk; only the text is copied to
+ * the host.  *bytes_written (nullable) = bytes written to fd. */
+int dqdk_gpu_histogram_write_csv(dqdk_gpu_queue_t* q, int fd, uint64_t* bytes_written);
+/* The JSON status line tristan_fini sends to the controller
+ * (src/tristan.c:171-189): events/bytes summed over the queues' counters,
+ * packets = sum of rcvd_pkts, runtime = max of runtime_ns[k] (nullable)
+ * in ms with 2 decimals.  Returns the snprintf length (truncates to bufsz). */
+int dqdk_gpu_tristan_summary(const dqdk_gpu_counters_t* const* per_queue, int nqueues, const uint64_t* runtime_ns,
+                             const char* directory, char* buf, uint64_t bufsz);
+
+/* ---- measurement helpers (membench.hip; not on the receive path) --------- */
+/* Streaming read of [d_buf, d_buf+bytes) (16-B aligned) on `stream`, and
+ * one relaxed device atomic increment of d_table[d_keys[i]] per key (keys
+ * >= entries skipped): iters timed passes after one warm-up, mean ms/pass. */
+int dqdk_gpu_membench_read(const void* d_buf, uint64_t bytes, void* stream, int iters, double* ms_per_pass);
+int dqdk_gpu_membench_atomic(uint32_t* d_table, uint64_t entries, const uint32_t* d_keys, uint64_t nkeys, void* stream,
+                             int iters, double* ms_per_pass);
+
 /* ---- stage timing (HIP events on the queue stream) ------------------------ */
-/* When enabled, every kernel of every batch is bracketed by hipEvents on the
- * queue stream; stage_ms[k] accumulates milliseconds for stage k
- * (0 = rx_decode, 1 = finalize, 2 = histogram), counts[k] = launches. */
+/* When enabled, every kernel launch of every batch is bracketed by its own
+ * pair of hipEvents on the queue stream; stage k is one kernel, named by
+ * dqdk_gpu_timing_stage_name(k):
+ *   0 rx_decode  1 rx_abort  2 rx_count  3 rx_histo_atomic
+ *   4 rx_part1   5 rx_hist_prep  6 rx_part2  7 rx_slice_histo
+ * timing_read adds up the completed pairs (after syncing the queue stream),
+ * writes stage_ms[k] / counts[k] (launches) for k < nstages and clears them. */
+#define DQDK_GPU_TIMING_STAGES 8
 int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on);
 int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages);
+const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
 
 const char* dqdk_gpu_last_error(void);
 

@@ -79,3 +79,14 @@ def test_synth_is_deterministic_and_seeded():
     f = u4.reshape(256, 4096)[0]
     assert f[12] == 8 and f[13] == 0 and f[14] == 0x45 and f[23] == 17
     assert (int(f[34]) << 8 | int(f[35])) == 5001 and (int(f[36]) << 8 | int(f[37])) == 5000
+
+
+def test_summary_line_matches_tristan_fini_format():
+    c = [{"total_events": 91, "total_bytes": 1458, "rcvd_pkts": 1},
+         {"total_events": 182, "total_bytes": 2916, "rcvd_pkts": 2}]
+    s = D.tristan_summary(c, [1_500_000, 2_250_000], "/data/run1")
+    # src/tristan.c:186-189
+    want = ("{ \"total_received_events\": %llu,\"total_received_bytes\": %llu, \"total_received_packets\": %llu, "
+            "\"dqdk_runtime_ms\": %.2lf, \"directory\": \"%s\"}").replace("%llu", "%d").replace("%.2lf", "%.2f") % (
+        273, 4374, 3, 2.25, "/data/run1")
+    assert s == want

@@ -1,0 +1,197 @@
+"""End-of-run egress on the GPU vs the reference's formats (tristan_fini,
+src/tristan.c:162-233): the histogram CSV formatted by the GPU, the
+controller JSON line, and the cross-queue merge helpers.
+
+Expected CSV text is produced here with the reference's own format strings
+(header src/tristan.c:198, lines :210 "%d,%d,%u,%u\\n") from the oracle's
+histogram of the same batch, so the file must match byte for byte.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import dqdk_amd as D
+from oracle import oracle as O
+from test_gpu_parity import _need_gpu, run_gpu
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+BINS_PER_HIST = 65536
+HEADER = "Channel,Histo,Energy,Freq\n"
+
+
+def ref_csv(keys: np.ndarray, counts: np.ndarray) -> str:
+    """The dprintf loop of src/tristan.c:203-213 over the non-zero bins."""
+    lines = [HEADER]
+    for k, c in zip(keys.tolist(), counts.tolist()):
+        ch, rest = divmod(int(k), 6 * BINS_PER_HIST)
+        h, e = divmod(rest, BINS_PER_HIST)
+        lines.append("%d,%d,%u,%u\n" % (ch, h, e, c))
+    return "".join(lines)
+
+
+def gpu_csv(q: D.RxQueue, tmp_path) -> str:
+    path = tmp_path / "histo.csv"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        n = q.write_histogram_csv(fd)
+    finally:
+        os.close(fd)
+    text = path.read_text()
+    assert n == len(text)
+    return text
+
+
+@pytest.mark.parametrize("hpath", [D.F_HISTO_ATOMIC, D.F_HISTO_PARTITIONED], ids=["atomic", "partitioned"])
+def test_histogram_csv_matches_reference_format(tmp_path, hpath):
+    _need_gpu()
+    umem, desc = D.synth_umem(4096, 1500, 4096, faulty=True)
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO, flags=D.F_CSUM | hpath)
+    q = D.RxQueue(0, cfg, len(desc))
+    try:
+        run_gpu(umem, desc, cfg, q=q)
+        ores, ocnt, okeys = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+        u, c = O.sparse_histogram(okeys, ores, cfg.events, None)
+        assert q.histogram_nonzero() == len(u)
+        assert gpu_csv(q, tmp_path) == ref_csv(u, c)
+    finally:
+        q.close()
+
+
+def test_histogram_csv_digit_widths_and_chunk_edges(tmp_path):
+    """Crafted table: first/last bin, CSV chunk edges (4M bins), every digit
+    width of channel, energy and count up to 0xFFFFFFFF."""
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO)
+    q = D.RxQueue(0, cfg, 1)
+    try:
+        rng = np.random.default_rng(7)
+        chunk = 1 << 22
+        idx = {0, 1, 9, 10, 99, 100, 65535, 65536, 6 * 65536 - 1, 6 * 65536, 10 * 6 * 65536 + 12345,
+               100 * 6 * 65536 + 99999 % 65536, 1000 * 6 * 65536 + 7, D.HISTO_ENTRIES - 1, D.HISTO_ENTRIES - 16,
+               chunk - 1, chunk, 2 * chunk - 1, 2 * chunk, 141 * chunk - 1, 141 * chunk}
+        idx |= set(rng.integers(0, D.HISTO_ENTRIES, 2000).tolist())
+        keys = np.array(sorted(idx), dtype=np.int64)
+        vals = np.array([1, 9, 10, 99, 100, 999, 1000, 65535, 65536, 10**6, 10**9 - 1, 10**9, 0xFFFFFFFF],
+                        dtype=np.uint64)
+        counts = vals[rng.integers(0, len(vals), len(keys))]
+        table = torch.zeros(D.HISTO_ENTRIES, dtype=torch.int32, device="cuda:0")
+        table[torch.from_numpy(keys).cuda()] = torch.from_numpy(counts.astype(np.uint32).view(np.int32)).cuda()
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        q.histogram_add(table.data_ptr())
+        q.histogram_add(table.data_ptr())  # u32 wrap: 2*0xFFFFFFFF -> 0xFFFFFFFE
+        torch.cuda.synchronize()
+        doubled = (counts * 2) & 0xFFFFFFFF
+        keep = doubled != 0
+        assert q.histogram_nonzero() == int(keep.sum())
+        assert gpu_csv(q, tmp_path) == ref_csv(keys[keep], doubled[keep])
+        # copy: table round-trips through a caller device buffer
+        out = torch.empty_like(table)
+        q.histogram_copy(out.data_ptr())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got[keys], doubled.astype(np.uint32))
+        assert int(np.count_nonzero(got)) == int(keep.sum())
+        del out, table
+    finally:
+        q.close()
+
+
+def test_empty_histogram_csv_is_header_only(tmp_path):
+    _need_gpu()
+    q = D.RxQueue(0, D.RxConfig(payloadsz=1458), 1)
+    try:
+        assert q.histogram_nonzero() == 0
+        assert gpu_csv(q, tmp_path) == HEADER
+    finally:
+        q.close()
+
+
+def test_merge_two_queues_equals_oracle_of_union():
+    """Per-GPU partial tables merged with copy+add equal one table over both
+    queues' frames (the end-of-run merge)."""
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
+    ua, da = D.synth_umem(2048, 1500, 4096, queue=0, faulty=True)
+    ub, db = D.synth_umem(2048, 1500, 4096, queue=1, faulty=True)
+    qa, qb = D.RxQueue(0, cfg, 2048), D.RxQueue(0, cfg, 2048)
+    try:
+        run_gpu(ua, da, cfg, q=qa)
+        run_gpu(ub, db, cfg, q=qb)
+        buf = torch.empty(D.HISTO_ENTRIES, dtype=torch.int32, device="cuda:0")
+        s = torch.cuda.current_stream().cuda_stream
+        qb.set_stream(s)
+        qa.set_stream(s)
+        qb.histogram_copy(buf.data_ptr())
+        qa.histogram_add(buf.data_ptr())
+        torch.cuda.synchronize()
+        hist = qa.histogram()
+        keys_all, res_all = [], []
+        for u, d in ((ua, da), (ub, db)):
+            r, _, k = O.rx_batch(u.copy(), d, cfg.payloadsz, cfg.mode, cfg.flags)
+            keys_all.append(k)
+            res_all.append(r)
+        uk, uc = O.sparse_histogram(np.concatenate(keys_all), np.concatenate(res_all), cfg.events, None)
+        nz = np.flatnonzero(hist)
+        np.testing.assert_array_equal(nz.astype(np.uint32), uk)
+        np.testing.assert_array_equal(hist[nz].astype(np.uint64), uc)
+        del buf
+    finally:
+        qa.close()
+        qb.close()
+
+
+def test_membench_helpers():
+    """The measured bounds bench.py quotes: streaming read and random atomics."""
+    _need_gpu()
+    import ctypes as C
+
+    from dqdk_amd import _lib as L
+    buf = torch.ones(1 << 26, dtype=torch.int32, device="cuda:0")  # 256 MB
+    ms = C.c_double()
+    s = torch.cuda.current_stream().cuda_stream
+    L.check(L.lib().dqdk_gpu_membench_read(buf.data_ptr(), buf.numel() * 4, s, 3, C.byref(ms)), "membench_read")
+    assert ms.value > 0
+    table = torch.zeros(1 << 20, dtype=torch.int32, device="cuda:0")
+    keys = torch.randint(0, (1 << 20) + 100, (1 << 22,), dtype=torch.int32, device="cuda:0")
+    L.check(L.lib().dqdk_gpu_membench_atomic(table.data_ptr(), 1 << 20, keys.data_ptr(), keys.numel(), s, 2,
+                                              C.byref(ms)), "membench_atomic")
+    torch.cuda.synchronize()
+    k = keys.cpu().numpy()
+    want = np.bincount(k[k < (1 << 20)], minlength=1 << 20) * 3  # warm-up + 2 passes
+    np.testing.assert_array_equal(table.cpu().numpy(), want)
+
+
+def test_fini_single_rank_rccl(tmp_path):
+    """dqdk_amd.multi.fini through a world-size-1 RCCL group: copy -> reduce ->
+    write-back leaves the table unchanged, and the CSV/JSON outputs match the
+    oracle of the queue's frames."""
+    _need_gpu()
+    import socket
+
+    import torch.distributed as dist
+
+    from dqdk_amd import multi
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    umem, desc = D.synth_umem(2048, 1500, 4096, faulty=True)
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO, flags=D.F_CSUM)
+    q = D.RxQueue(0, cfg, len(desc))
+    try:
+        run_gpu(umem, desc, cfg, q=q)
+        path = tmp_path / "histo.csv"
+        line = multi.fini(q, 3_000_000, str(tmp_path), str(path))
+        ores, ocnt, okeys = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+        u, c = O.sparse_histogram(okeys, ores, cfg.events, None)
+        assert path.read_text() == ref_csv(u, c)
+        assert line == D.tristan_summary([ocnt], [3_000_000], str(tmp_path))
+        assert f'"total_received_packets": {ocnt["rcvd_pkts"]}' in line
+    finally:
+        q.close()
+        dist.destroy_process_group()

@@ -1,17 +1,17 @@
 #!/bin/bash
-# rocprofv3 PMC passes (one counter group per pass, no tracing flags) over a
-# short bench run.  usage (on the GPU box): bash tools/pmc.sh <tag> [bench args...]
+# rocprofv3 PMC passes (one counter group per pass, kernel-trace only, no
+# tracing domains) over a short bench run, then the per-kernel summary into
+# gpurun_out/pmc_summary.json under bench.py's workload key.
+# usage (on the GPU box): bash tools/pmc.sh <tag> <frame_len> [bench args...]
 set -e
-tag=${1:-run}; shift || true
+tag=${1:-run}; L=${2:-1500}; shift 2 || true
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/pmc_$tag
-rocprofv3 -L > gpurun_out/pmc_$tag/counters_available.txt 2>&1 || true
+d=gpurun_out/pmc_${tag}_$L
+mkdir -p $d
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-           "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU" \
-           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD"; do
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_$tag/p$i -o run --output-format csv -- \
-        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/pmc_$tag/p$i.log 2>&1 || \
-        echo "pass $i ($grp) failed rc=$?" >> gpurun_out/pmc_$tag/errors.txt
+    timeout -k 10 300 rocprofv3 --pmc $grp -d $d/p$i -o run --output-format csv -- \
+        python3 bench.py --frame-len $L --steps 3 --warmup 1 --no-cpu-baseline "$@" > $d/p$i.log 2>&1
 done
+python3 tools/pmc_summary.py $d gpurun_out/pmc_summary.json "$L:csum:1048576" > $d/summary.txt

@@ -1,7 +1,11 @@
 """Summarise rocprofv3 PMC passes (tools/pmc.sh) per kernel: mean per dispatch.
 
 FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 reports half the
-bytes of wide coalesced reads); both sizes are in KB per rocprofv3."""
+bytes of wide coalesced reads); FETCH_SIZE / WRITE_SIZE are in KB.
+
+usage: python tools/pmc_summary.py <pmc dir> [<summary.json> <workload key>]
+The workload key is the one bench.py looks up: "<frame_len>:<csum|nocsum>:<frames>".
+"""
 import csv
 import json
 import sys
@@ -11,10 +15,9 @@ from pathlib import Path
 
 def load(d: Path):
     acc = defaultdict(lambda: defaultdict(list))
-    for f in sorted(d.glob("p*/run_counter_collection.csv")):
+    for f in sorted(d.glob("p*/**/*counter_collection.csv")):
         with open(f) as fh:
             rows = list(csv.DictReader(fh))
-        # one row per (dispatch, counter)
         per = defaultdict(lambda: defaultdict(float))
         names = {}
         for r in rows:
@@ -27,26 +30,36 @@ def load(d: Path):
     return acc
 
 
-def main():
-    d = Path(sys.argv[1])
-    acc = load(d)
+def summarise(d: Path) -> dict:
     out = {}
-    for k, cs in acc.items():
-        short = k.split("(")[0].replace("dqdk::", "")
+    for k, cs in load(d).items():
+        short = k.split("(")[0].replace("dqdk::", "").replace("void ", "").strip()
         m = {c: sum(v) / len(v) for c, v in cs.items()}
+        m["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in m:
             m["hbm_read_bytes_corrected"] = m["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in m:
             m["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            m["hbm_bytes_per_launch"] = m["hbm_read_bytes_corrected"] + m["hbm_write_bytes"]
         out[short] = m
+    return out
+
+
+def main():
+    d = Path(sys.argv[1])
+    out = summarise(d)
     for k, m in sorted(out.items()):
         if not k.startswith("rx_"):
             continue
         print(k)
         for c, v in sorted(m.items()):
             print(f"   {c:32s} {v:16.4g}")
-    if len(sys.argv) > 2:
-        Path(sys.argv[2]).write_text(json.dumps(out, indent=1))
+    if len(sys.argv) > 3:
+        p = Path(sys.argv[2])
+        allw = json.loads(p.read_text()) if p.exists() else {}
+        allw[sys.argv[3]] = {k: v for k, v in out.items() if k.startswith("rx_")}
+        p.write_text(json.dumps(allw, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
