@@ -195,7 +195,7 @@ def main():
     try:
         pmc = json.loads(Path(args.pmc).read_text())
         w = pmc.get(f"{L}:{'csum' if not args.no_csum else 'nocsum'}:{n}", {})
-        traffic = w.get("rx_decode", {}).get("hbm_bytes_per_launch")
+        traffic = w.get("rx_decode_kernel", {}).get("hbm_bytes_per_launch")
     except Exception:
         pass
     dec = st.get("rx_decode", {})

@@ -93,6 +93,13 @@ struct dqdk_gpu_queue {
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     dqdk_gpu_desc_t* d_desc = nullptr;
     dqdk_gpu_rx_result_t* d_res = nullptr;
+    // raw payload stream (tristan.c:318-324)
+    int raw_fd = -1;
+    uint64_t* d_raw_blk = nullptr;  // per-256-frame byte totals -> offsets
+    uint8_t* d_raw = nullptr;       // host drop-in staging
+    uint64_t raw_cap = 0;
+    uint8_t* h_raw = nullptr;       // pinned
+    uint64_t h_raw_cap = 0;
     std::vector<Reg> regs;
     // stage timing
     int timing = 0;
@@ -244,6 +251,82 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     return 0;
 }
 
+// Enqueue the raw payload gather of the batch just launched on q->stream;
+// the byte total lands in q->d_raw_blk[nblk].
+int launch_raw(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc, uint32_t n,
+               const dqdk_gpu_rx_result_t* d_res, uint8_t* d_out, uint64_t out_cap, bool copy)
+{
+    RawArgs ra{};
+    ra.umem = d_umem;
+    ra.umem_size = umem_size;
+    ra.desc = d_desc;
+    ra.res = d_res;
+    ra.n = n;
+    ra.flags = q->cfg.flags;
+    ra.batch_scratch = q->d_batch;
+    ra.blk = q->d_raw_blk;
+    ra.out = d_out;
+    ra.out_cap = out_cap;
+    const uint32_t nblk = (n + kRawThreads - 1) / kRawThreads;
+    hipLaunchKernelGGL(raw_len_kernel, dim3(nblk), dim3(kRawThreads), 0, q->stream, ra);
+    hipLaunchKernelGGL(csv_scan_kernel, dim3(1), dim3(1024), 0, q->stream, q->d_raw_blk, nblk);
+    if (copy)
+        hipLaunchKernelGGL(raw_copy_kernel, dim3(nblk), dim3(kRawThreads), 0, q->stream, ra);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int raw_total(dqdk_gpu_queue* q, uint32_t n, uint64_t* total)
+{
+    const uint32_t nblk = (n + kRawThreads - 1) / kRawThreads;
+    HIPCHK(hipMemcpyAsync(total, q->d_raw_blk + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost, q->stream));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    return 0;
+}
+
+// Host drop-in: append the batch's raw payload stream to q->raw_fd.
+int write_raw(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint32_t n)
+{
+    int rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, nullptr, 0, false);
+    uint64_t total = 0;
+    if (!rc)
+        rc = raw_total(q, n, &total);
+    if (rc || !total)
+        return rc;
+    if (total > q->raw_cap) {
+        (void)hipFree(q->d_raw);
+        q->d_raw = nullptr;
+        q->raw_cap = 0;
+        HIPCHK(hipMalloc(&q->d_raw, total));
+        q->raw_cap = total;
+    }
+    if (total > q->h_raw_cap) {
+        if (q->h_raw)
+            (void)hipHostFree(q->h_raw);
+        q->h_raw = nullptr;
+        q->h_raw_cap = 0;
+        HIPCHK(hipHostMalloc(&q->h_raw, total, hipHostMallocDefault));
+        q->h_raw_cap = total;
+    }
+    rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, q->d_raw, q->raw_cap, true);
+    if (rc)
+        return rc;
+    HIPCHK(hipMemcpyAsync(q->h_raw, q->d_raw, total, hipMemcpyDeviceToHost, q->stream));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    for (uint64_t o = 0; o < total;) {
+        const ssize_t w = write(q->raw_fd, q->h_raw + o, total - o);
+        if (w < 0) {
+            if (errno == EINTR)
+                continue;
+            const int err = errno;
+            g_err = std::string("raw write: ") + strerror(err);
+            return -err;
+        }
+        o += (uint64_t)w;
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -303,7 +386,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     if ((e = hipMalloc(&q->d_cum, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_batch, kBatchScratch * sizeof(uint64_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_desc, (size_t)max_batch * sizeof(dqdk_gpu_desc_t))) != hipSuccess ||
-        (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess)
+        (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess ||
+        (e = hipMalloc(&q->d_raw_blk, ((size_t)max_batch / kRawThreads + 2) * sizeof(uint64_t))) != hipSuccess)
         return cleanup((fail("hipMalloc", e), -ENOMEM));
     if ((e = hipMemset(q->d_cum, 0, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
@@ -352,6 +436,10 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_hscratch);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
+    (void)hipFree(q->d_raw_blk);
+    (void)hipFree(q->d_raw);
+    if (q->h_raw)
+        (void)hipHostFree(q->h_raw);
     if (q->own_stream)
         (void)hipStreamDestroy(q->own_stream);
     delete q;
@@ -460,6 +548,8 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
     int rc = launch_batch(q, dev_umem, umem_size, q->d_desc, n, q->d_res, nullptr);
     if (rc)
         return rc;
+    if (q->raw_fd >= 0 && (rc = write_raw(q, dev_umem, umem_size, n)) != 0)
+        return rc;
     HIPCHK(hipMemcpyAsync(per_pkt, q->d_res, (size_t)n * sizeof(*per_pkt), hipMemcpyDeviceToHost, q->stream));
     uint64_t b[kBatchScratch];
     HIPCHK(hipMemcpyAsync(b, q->d_batch, sizeof(b), hipMemcpyDeviceToHost, q->stream));
@@ -563,6 +653,34 @@ int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts
         q->stage_ms[k] = 0;
         q->counts[k] = 0;
     }
+    return 0;
+}
+
+int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
+                                const dqdk_gpu_desc_t* d_desc, uint32_t n, const dqdk_gpu_rx_result_t* d_results,
+                                uint8_t* d_out, uint64_t out_cap, uint64_t* total)
+{
+    if (!q || !d_umem || !d_desc || !d_results || (!d_out && out_cap))
+        return fail_errno(-EINVAL, "raw_compact_device: null argument");
+    if (n > q->max_batch)
+        return fail_errno(-EINVAL, "raw_compact_device: n > max_batch");
+    if (n == 0) {
+        if (total)
+            *total = 0;
+        return 0;
+    }
+    HIPCHK(hipSetDevice(q->device));
+    int rc = launch_raw(q, d_umem, umem_size, d_desc, n, d_results, d_out, out_cap, d_out != nullptr);
+    if (!rc && total)
+        rc = raw_total(q, n, total);
+    return rc;
+}
+
+int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)
+{
+    if (!q)
+        return -EINVAL;
+    q->raw_fd = fd;
     return 0;
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/dqdk_gpu.h"
+
 namespace dqdk {
 
 constexpr int kCsvThreads = 256;
@@ -15,6 +17,23 @@ constexpr uint64_t kCsvMaxLine = 4 + 1 + 1 + 1 + 5 + 1 + 10 + 1;  // "1511,5,655
 __global__ void csv_len_kernel(const uint32_t* hist, uint64_t base, uint64_t end, uint64_t* blk_chars);
 __global__ void csv_scan_kernel(uint64_t* blk_chars, uint32_t nblk);
 __global__ void csv_write_kernel(const uint32_t* hist, uint64_t base, uint64_t end, const uint64_t* blk_off, char* out);
+// Raw payload stream (tristan_process write(), src/tristan.c:318-324)
+constexpr int kRawThreads = 256;  // frames per block in the scan passes
+struct RawArgs {
+    const uint8_t* umem;
+    uint64_t umem_size;
+    const dqdk_gpu_desc_t* desc;
+    const dqdk_gpu_rx_result_t* res;
+    uint32_t n;
+    uint32_t flags;
+    const uint64_t* batch_scratch;  // [0] = first abort index of the batch
+    uint64_t* blk;                  // [nblk + 1] block byte totals -> offsets, [nblk] = total
+    uint8_t* out;
+    uint64_t out_cap;
+};
+__global__ void raw_len_kernel(RawArgs a);
+__global__ void raw_copy_kernel(RawArgs a);
+
 __global__ void hist_add_kernel(uint32_t* dst, const uint32_t* src, uint64_t n16);
 __global__ void hist_nonzero_kernel(const uint32_t* hist, uint64_t n16, unsigned long long* count);
 

@@ -171,6 +171,101 @@ __global__ __launch_bounds__(kCsvThreads) void csv_write_kernel(const uint32_t* 
     }
 }
 
+// ---- raw payload stream -------------------------------------------------------
+// Bytes frame i contributes: its datalen if it is an accounted OK frame (the
+// frames process_frame hands to tristan_process, src/dqdk.c:243-247) whose
+// payload lies inside the UMEM; 0 otherwise.  A u32-wrapped datalen (udplen
+// < 8, src/dqdk.c:205) would make the reference write() ~4 GB from the frame
+// and fail; such frames contribute nothing here.
+__device__ __forceinline__ uint64_t raw_bytes(const RawArgs& a, uint32_t i, uint32_t limit, uint64_t* src)
+{
+    if (i >= limit)
+        return 0;
+    const dqdk_gpu_rx_result_t r = a.res[i];
+    if (r.status != DQDK_RX_OK)
+        return 0;
+    const uint64_t p = a.desc[i].addr + r.payload_off;
+    if (p > a.umem_size || r.datalen > a.umem_size - p)
+        return 0;
+    *src = p;
+    return r.datalen;
+}
+
+__device__ __forceinline__ uint32_t raw_limit(const RawArgs& a)
+{
+    const uint64_t abort_idx = a.batch_scratch[0];
+    return (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (uint32_t)(abort_idx < a.n ? abort_idx : a.n) : a.n;
+}
+
+__global__ __launch_bounds__(kRawThreads) void raw_len_kernel(RawArgs a)
+{
+    __shared__ uint64_t lds[kRawThreads / 64];
+    const uint32_t i = blockIdx.x * kRawThreads + threadIdx.x;
+    uint64_t src = 0;
+    const uint64_t b = raw_bytes(a, i, min(raw_limit(a), a.n), &src);
+    uint64_t total;
+    (void)block_excl_scan<uint64_t>(b, lds, &total);
+    if (threadIdx.x == 0)
+        a.blk[blockIdx.x] = total;
+}
+
+// One wave per frame of the block: 4-B output words, each assembled from two
+// aligned source words with alignbyte; the partial words at both ends of a
+// frame's output are written bytewise (they are shared with the neighbours).
+__global__ __launch_bounds__(kRawThreads) void raw_copy_kernel(RawArgs a)
+{
+    __shared__ uint64_t lds[kRawThreads / 64];
+    __shared__ uint64_t s_off[kRawThreads], s_src[kRawThreads];
+    __shared__ uint32_t s_len[kRawThreads];
+    const uint32_t i = blockIdx.x * kRawThreads + threadIdx.x;
+    uint64_t src = 0;
+    const uint64_t b = raw_bytes(a, i, min(raw_limit(a), a.n), &src);
+    uint64_t total;
+    const uint64_t off = a.blk[blockIdx.x] + block_excl_scan<uint64_t>(b, lds, &total);
+    s_off[threadIdx.x] = off;
+    s_src[threadIdx.x] = src;
+    s_len[threadIdx.x] = (uint32_t)b;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.umem, (short)0, (int)(a.umem_size > 0x7fffffffull ? 0x7fffffffull : a.umem_size), 0x00020000);
+    for (int f = w; f < kRawThreads; f += kRawThreads / 64) {
+        const uint64_t D = s_off[f], S = s_src[f];
+        uint64_t len = s_len[f];
+        if (D >= a.out_cap)
+            continue;
+        if (len > a.out_cap - D)
+            len = a.out_cap - D;
+        if (!len)
+            continue;
+        const uint64_t E = D + len;
+        const uint64_t k0 = D >> 2, k1 = (E + 3) >> 2;  // output words touched
+        for (uint64_t k = k0 + lane; k < k1; k += 64) {
+            const uint64_t d = k << 2;        // first byte of the word
+            const int64_t s = (int64_t)S + (int64_t)(d - D);  // source of byte d (may precede S for k0)
+            const uint64_t sa = (uint64_t)(s & ~3ll);
+            const uint32_t sh = (uint32_t)(s & 3);
+            uint32_t w0, w1;
+            if (S < 0x7ffffff0ull) {
+                w0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)sa, 0, 0);
+                w1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)sa + 4u, 0, 0);
+            } else {
+                w0 = *(const uint32_t*)(a.umem + sa);
+                w1 = sa + 8 <= a.umem_size ? *(const uint32_t*)(a.umem + sa + 4) : 0u;
+            }
+            const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            if (d >= D && d + 4 <= E) {
+                *(uint32_t*)(a.out + d) = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (d + j >= D && d + j < E)
+                        a.out[d + j] = (uint8_t)(v >> (8 * j));
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void hist_add_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t n16)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;

@@ -360,19 +360,26 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
     const int c = c0 + lane;
     const bool inr = active && c < P.c_end;
     if (P.work & 2) {
-        const uint32_t M = 0x00ff00ffu;  // bytes at even positions (chunk starts are 4-aligned)
-        uint32_t te = (v.x & M) + (v.y & M) + (v.z & M) + (v.w & M);
-        uint32_t to = ((v.x >> 8) & M) + ((v.y >> 8) & M) + ((v.z >> 8) & M) + ((v.w >> 8) & M);
+        // even- / odd-position byte sums with one dot4 per dword each (chunk
+        // starts are 4-aligned relative to the frame, so byte parity = the
+        // position in the dword); lanes outside the checksum range get zero weights
         const bool incs = inr && c <= P.ct;
-        te = incs ? te : 0u;
-        to = incs ? to : 0u;
+        const uint32_t we = incs ? 0x00010001u : 0u, wo = incs ? 0x01000100u : 0u;
+        acc_e = __builtin_amdgcn_udot4(v.x, we, acc_e, false);
+        acc_o = __builtin_amdgcn_udot4(v.x, wo, acc_o, false);
+        acc_e = __builtin_amdgcn_udot4(v.y, we, acc_e, false);
+        acc_o = __builtin_amdgcn_udot4(v.y, wo, acc_o, false);
+        acc_e = __builtin_amdgcn_udot4(v.z, we, acc_e, false);
+        acc_o = __builtin_amdgcn_udot4(v.z, wo, acc_o, false);
+        acc_e = __builtin_amdgcn_udot4(v.w, we, acc_e, false);
+        acc_o = __builtin_amdgcn_udot4(v.w, wo, acc_o, false);
         if (active) {
             // uniform: the first checksum chunk (lane 0 of window 0) and the
             // last one (chunk ct) may hold bytes outside [cs_lo, cs_hi)
             // (cs_hi includes the odd-length over-read byte); their sums are
             // taken from the owning lane's data in SGPRs and subtracted from
             // the frame total at its end
-            if (w == 0) {
+            if (w == 0 && P.ct >= P.c_begin) {  // (ct < c_begin: no checksum bytes at all)
                 const int nb = P.cs_lo - (16 * P.c_begin + P.q4);
                 if (nb > 0) {
                     uint32_t de, dd;
@@ -393,8 +400,6 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
                 }
             }
         }
-        acc_e += (te & 0xffff) + (te >> 16);
-        acc_o += (to & 0xffff) + (to >> 16);
     }
     if (P.work & 1) {
         const uint32_t e = (uint32_t)(c - P.ce0);

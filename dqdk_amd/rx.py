@@ -127,6 +127,19 @@ class RxQueue:
                                           res.ctypes.data, C.byref(delta)), "dqdk_gpu_rx_batch")
         return res, delta.as_dict()
 
+    def raw_compact_device(self, umem_ptr: int, umem_size: int, desc_ptr: int, n: int, results_ptr: int,
+                           out_ptr: int | None = None, out_cap: int = 0, sync: bool = True) -> int | None:
+        """Gather the batch's raw payload stream (src/tristan.c:318-324) on the GPU."""
+        tot = C.c_uint64()
+        L.check(L.lib().dqdk_gpu_raw_compact_device(self._h, umem_ptr, umem_size, desc_ptr, n, results_ptr,
+                                                    out_ptr or None, out_cap, C.byref(tot) if sync else None),
+                "raw_compact_device")
+        return int(tot.value) if sync else None
+
+    def set_raw_fd(self, fd: int) -> None:
+        """Append every host batch's raw payload stream to fd (-1 = off)."""
+        L.check(L.lib().dqdk_gpu_queue_set_raw_fd(self._h, fd), "set_raw_fd")
+
     def register_umem(self, umem: np.ndarray) -> None:
         L.check(L.lib().dqdk_gpu_umem_register(self._h, umem.ctypes.data, umem.nbytes), "umem_register")
 

@@ -156,6 +156,23 @@ int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
 int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,
                       uint32_t n, dqdk_gpu_rx_result_t* per_pkt, dqdk_gpu_counters_t* delta);
 
+/* ---- raw payload stream (tristan_process write(), src/tristan.c:318-324) -- */
+/* The concatenation, in descriptor order, of payload[0, datalen) of every
+ * frame the batch hands to the frame processor (accounted OK frames; in
+ * BATCH_ABORT mode those before the first failure) -- what the reference
+ * writes to its raw file when rawdata_fd >= 0 (waveform mode always).
+ * Frames whose u32-wrapped datalen runs past the UMEM contribute nothing.
+ * Device form: call after dqdk_gpu_rx_batch_device on the same queue stream
+ * with the same d_desc/d_results; writes min(total, out_cap) bytes to d_out
+ * (NULL with out_cap 0 = size query).  total (host, nullable) = the stream's
+ * full length, which makes the call synchronous.  Host form: with a raw fd
+ * set, dqdk_gpu_rx_batch appends each batch's stream to it (GPU gather, one
+ * D2H copy, write()). */
+int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
+                                const dqdk_gpu_desc_t* d_desc, uint32_t n, const dqdk_gpu_rx_result_t* d_results,
+                                uint8_t* d_out, uint64_t out_cap, uint64_t* total);
+int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd); /* -1 = off (default) */
+
 /* ---- counters / histogram egress ----------------------------------------- */
 int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out); /* cumulative */
 int dqdk_gpu_counters_reset(dqdk_gpu_queue_t* q);

@@ -195,3 +195,77 @@ def test_fini_single_rank_rccl(tmp_path):
     finally:
         q.close()
         dist.destroy_process_group()
+
+
+def ref_raw(umem, desc, ores, ocnt, flags) -> bytes:
+    """tristan_process's write(rawdata_fd, payload, datalen) for every frame
+    process_frame hands over (src/tristan.c:318-324, src/dqdk.c:243-247).
+    A u32-wrapped datalen (udplen < 8: the synthetic SHORT frames) would make
+    the reference write() ~4 GB past the frame and fail; such frames, whose
+    payload runs past the UMEM, contribute nothing (include/dqdk_gpu.h)."""
+    limit = ocnt["first_abort_idx"] if flags & D.F_BATCH_ABORT else len(desc)
+    out = []
+    for i in range(min(limit, len(desc))):
+        if ores["status"][i] == D.RX_OK:
+            p = int(desc["addr"][i]) + int(ores["payload_off"][i])
+            n = int(ores["datalen"][i])
+            if p + n <= umem.nbytes:
+                out.append(umem[p : p + n].tobytes())
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("flags", [0, D.F_CSUM, D.F_CSUM | D.F_BATCH_ABORT])
+@pytest.mark.parametrize("L,stride,mode", [(1500, 4096, D.MODE_WAVEFORM), (0, 9216, D.MODE_LISTMODE),
+                                           (1500, 1501, D.MODE_ENERGYHISTO)])
+def test_raw_stream_device_matches_reference(L, stride, mode, flags):
+    _need_gpu()
+    umem, desc = D.synth_umem(3000, L, stride, faulty=True)
+    cfg = D.RxConfig(payloadsz=1458, mode=mode, flags=flags)
+    ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+    want = ref_raw(umem, desc, ores, ocnt, flags)
+    q = D.RxQueue(0, cfg, len(desc))
+    try:
+        d_umem = torch.from_numpy(umem).cuda()
+        d_desc = torch.from_numpy(desc.view(np.uint8)).cuda()
+        d_res = torch.zeros(len(desc) * 8, dtype=torch.uint8, device="cuda:0")
+        d_keys = torch.zeros(max(len(desc) * cfg.events, 1), dtype=torch.int32, device="cuda:0")
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        args = (d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), len(desc), d_res.data_ptr())
+        q.process_device(*args, d_keys.data_ptr())
+        assert q.raw_compact_device(*args) == len(want)  # size query
+        out = torch.full((len(want) + 64,), 0xAB, dtype=torch.uint8, device="cuda:0")
+        assert q.raw_compact_device(*args, out.data_ptr(), len(want)) == len(want)
+        got = out.cpu().numpy()
+        assert got[: len(want)].tobytes() == want
+        assert (got[len(want):] == 0xAB).all()  # nothing past the stream
+        # a short buffer gets exactly its capacity
+        cap = len(want) // 3 + 1
+        out[:] = 0xAB
+        assert q.raw_compact_device(*args, out.data_ptr(), cap) == len(want)
+        got = out.cpu().numpy()
+        assert got[:cap].tobytes() == want[:cap] and (got[cap:] == 0xAB).all()
+    finally:
+        q.close()
+
+
+def test_raw_stream_host_dropin_appends_to_fd(tmp_path):
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM)
+    path = tmp_path / "raw.bin"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    q = D.RxQueue(0, cfg, 2048)
+    want = []
+    try:
+        q.set_raw_fd(fd)
+        for b in range(3):
+            umem, desc = D.synth_umem(2048, 1500, 4096, queue=b, faulty=True)
+            res, _ = q.process_batch(umem, desc)
+            ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+            np.testing.assert_array_equal(res["status"], ores["status"])
+            want.append(ref_raw(umem, desc, ores, ocnt, cfg.flags))
+            q.unregister_umem(umem)
+        q.set_raw_fd(-1)
+    finally:
+        q.close()
+        os.close(fd)
+    assert path.read_bytes() == b"".join(want)
