@@ -565,9 +565,20 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
 
+    // Waves take 64-frame tiles from the batch's dispenser until it is
+    // exhausted; the grid is what fits on the GPU at once, so there is no
+    // second round of blocks and the load balances itself.
+    (void)wave;
     const uint32_t ntiles = (a.n + 63) / 64;
-    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves)
-        decode_wave_tile(a, t, lane, lds_cnt1);
+    for (;;) {
+        unsigned long long g = 0;
+        if (lane == 0)
+            g = atomicAdd(a.tile_ctr, 1ull);
+        const uint64_t t = ((uint64_t)rfl((uint32_t)(g >> 32)) << 32) | rfl((uint32_t)g);
+        if (t >= ntiles)
+            break;
+        decode_wave_tile(a, (uint32_t)t, lane, lds_cnt1);
+    }
 
     if (a.cnt1) {
         __syncthreads();
