@@ -90,8 +90,6 @@ struct dqdk_gpu_queue {
     uint16_t* d_part2 = nullptr;
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
-    unsigned long long* d_tile_ctr = nullptr;  // rx_decode tile dispenser
-    uint32_t decode_grid = 0;                  // rx_decode blocks resident at once
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     dqdk_gpu_desc_t* d_desc = nullptr;
     dqdk_gpu_rx_result_t* d_res = nullptr;
@@ -179,13 +177,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ra.batch_scratch = q->d_batch;
     const bool partitioned = q->histo && q->E && use_partitioned(q, n);
     ra.cnt1 = partitioned ? q->d_hscratch + kOffCnt1 : nullptr;
-    ra.tile_ctr = q->d_tile_ctr;
     if (partitioned)
         HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
     const uint32_t nblk = (n + kTile - 1) / kTile;
-    const uint32_t grid_dec = std::min<uint32_t>(nblk, q->decode_grid);
-    HIPCHK(hipMemsetAsync(q->d_tile_ctr, 0, sizeof(unsigned long long), q->stream));
+    const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * 8u);
     {
         StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_decode_kernel, dim3(grid_dec), dim3(kTile), 0, q->stream, ra);
@@ -393,16 +389,6 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_raw_blk, ((size_t)max_batch / kRawThreads + 2) * sizeof(uint64_t))) != hipSuccess)
         return cleanup((fail("hipMalloc", e), -ENOMEM));
-    if ((e = hipMalloc(&q->d_tile_ctr, sizeof(unsigned long long))) != hipSuccess)
-        return cleanup((fail("hipMalloc", e), -ENOMEM));
-    if ((e = hipMemset(q->d_tile_ctr, 0, sizeof(unsigned long long))) != hipSuccess)
-        return cleanup(fail("hipMemset", e));
-    {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rx_decode_kernel, kTile, 0) != hipSuccess || per_cu < 1)
-            per_cu = 4;
-        q->decode_grid = (uint32_t)per_cu * (uint32_t)q->cu_count;
-    }
     if ((e = hipMemset(q->d_cum, 0, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));
@@ -448,7 +434,6 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_part2);
     (void)hipFree(q->d_runs);
     (void)hipFree(q->d_hscratch);
-    (void)hipFree(q->d_tile_ctr);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     (void)hipFree(q->d_raw_blk);

@@ -66,7 +66,6 @@ struct RxArgs {
     uint32_t port_start, port_end;
     uint64_t* batch_scratch;  // [0] = first abort idx, [1..12] = per-batch counters
     uint32_t* cnt1;           // partitioned histogram: bucket counts (+ KEY_NONE records for non-OK frames), or null
-    unsigned long long* tile_ctr;  // 64-frame tile dispenser, zeroed before each batch
 };
 
 struct CountArgs {

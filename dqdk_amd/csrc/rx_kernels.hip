@@ -9,6 +9,11 @@ namespace dqdk {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// (a helper taking the dword by value: __builtin_bit_cast applied directly
+// to an ext_vector element such as v.y reads element 0 with hipcc 7.2)
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 
 // Byte layout constants (src/tristan.h:55-60).
 constexpr uint32_t kChannels = DQDK_TRISTAN_CHANNELS;
@@ -352,27 +357,22 @@ __device__ __forceinline__ void wave_frame(const RxArgs& a, const LaneFrame& lf,
 // of the events whose byte 2 falls in each lane's chunk.
 __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame& P, uint32_t slot, int w,
                                                const u32x4& v, int lane, bool active,
-                                               __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc_e,
-                                               uint32_t& acc_o, uint32_t& corr_e, uint32_t& corr_o, uint32_t& oob,
-                                               uint32_t* lds_cnt1)
+                                               __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc, uint32_t& corr,
+                                               uint32_t& oob, uint32_t* lds_cnt1)
 {
     const int c0 = P.c_begin + 64 * w;
     const int c = c0 + lane;
     const bool inr = active && c < P.c_end;
     if (P.work & 2) {
-        // even- / odd-position byte sums with one dot4 per dword each (chunk
-        // starts are 4-aligned relative to the frame, so byte parity = the
-        // position in the dword); lanes outside the checksum range get zero weights
+        // T = sum of the LE 16-bit words at even addresses (chunk starts are
+        // 4-aligned, so a dword's two halves): one dot2 per dword; lanes
+        // outside the checksum range get zero weights
         const bool incs = inr && c <= P.ct;
-        const uint32_t we = incs ? 0x00010001u : 0u, wo = incs ? 0x01000100u : 0u;
-        acc_e = __builtin_amdgcn_udot4(v.x, we, acc_e, false);
-        acc_o = __builtin_amdgcn_udot4(v.x, wo, acc_o, false);
-        acc_e = __builtin_amdgcn_udot4(v.y, we, acc_e, false);
-        acc_o = __builtin_amdgcn_udot4(v.y, wo, acc_o, false);
-        acc_e = __builtin_amdgcn_udot4(v.z, we, acc_e, false);
-        acc_o = __builtin_amdgcn_udot4(v.z, wo, acc_o, false);
-        acc_e = __builtin_amdgcn_udot4(v.w, we, acc_e, false);
-        acc_o = __builtin_amdgcn_udot4(v.w, wo, acc_o, false);
+        const u16x2 wt = incs ? u16x2{1, 1} : u16x2{0, 0};
+        acc = __builtin_amdgcn_udot2(as_u16x2(v.x), wt, acc, false);
+        acc = __builtin_amdgcn_udot2(as_u16x2(v.y), wt, acc, false);
+        acc = __builtin_amdgcn_udot2(as_u16x2(v.z), wt, acc, false);
+        acc = __builtin_amdgcn_udot2(as_u16x2(v.w), wt, acc, false);
         if (active) {
             // uniform: the first checksum chunk (lane 0 of window 0) and the
             // last one (chunk ct) may hold bytes outside [cs_lo, cs_hi)
@@ -384,8 +384,7 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
                 if (nb > 0) {
                     uint32_t de, dd;
                     chunk_range_sums(rdl(v.x, 0), rdl(v.y, 0), rdl(v.z, 0), rdl(v.w, 0), 0, nb, de, dd);
-                    corr_e += de;
-                    corr_o += dd;
+                    corr += de + 256u * dd;
                 }
             }
             const int lt = P.ct - c0;
@@ -395,8 +394,7 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
                     const uint32_t l = (uint32_t)lt;
                     uint32_t de, dd;
                     chunk_range_sums(rdl(v.x, l), rdl(v.y, l), rdl(v.z, l), rdl(v.w, l), keep, 16, de, dd);
-                    corr_e += de;
-                    corr_o += dd;
+                    corr += de + 256u * dd;
                 }
             }
         }
@@ -415,7 +413,7 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame&
         __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + e) * 4u : kOOB, 0, 0);
         if (a.cnt1)  // capacity of the key's L1 bucket (slot kL1Buckets absorbs the rest)
             atomicAdd(&lds_cnt1[has_evt && !bad ? (key >> kL1Shift) : (uint32_t)kL1Buckets], 1u);
-        oob += (has_evt && bad) ? 1u : 0u;  // per lane; summed at the frame's end
+        oob += (uint32_t)__builtin_popcountll(__ballot(has_evt && bad));  // wave-uniform
     }
 }
 
@@ -445,7 +443,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     lf.work = stream ? fi.work : 0u;
 
     // ---- phase B: stream the payloads ----
-    uint32_t sum_e = 0, sum_o = 0, sum_oob = 0;  // this lane's frame, written by the owner loop
+    uint32_t sum_t = 0, sum_oob = 0;  // this lane's frame, written by the owner loop
     const uint64_t smask0 = __ballot(stream);
     if (smask0) {
         const int total = (int)wave_sum_dpp(stream ? (uint32_t)lf.g.nwin : 0u);
@@ -480,26 +478,21 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
         int wp = 0;
         WaveFrame P;
         wave_frame(a, lf, jp, false, P);
-        uint32_t acc_e = 0, acc_o = 0, oob = 0, corr_e = 0, corr_o = 0;
+        uint32_t acc = 0, corr = 0, oob = 0;  // acc per lane; corr, oob wave-uniform
         for (int k = 0; k < total; k += kRing) {
 #pragma unroll
             for (int d = 0; d < kRing; d++) {
                 const bool active = k + d < total;
-                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc_e, acc_o, corr_e, corr_o, oob,
-                               lds_cnt1);
+                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc, corr, oob, lds_cnt1);
                 if (active && ++wp == P.nwin) {
                     // hand the frame's totals to its owning lane
                     const bool owner = lane == (int)jp;
                     if (P.work & 2) {
-                        const uint32_t se = wave_sum_dpp(acc_e) - corr_e, so = wave_sum_dpp(acc_o) - corr_o;
-                        sum_e = owner ? se : sum_e;
-                        sum_o = owner ? so : sum_o;
+                        const uint32_t t = wave_sum_dpp(acc) - corr;
+                        sum_t = owner ? t : sum_t;
                     }
-                    if (P.work & 1) {
-                        const uint32_t so = wave_sum_dpp(oob);
-                        sum_oob = owner ? so : sum_oob;
-                    }
-                    acc_e = acc_o = oob = corr_e = corr_o = 0;
+                    sum_oob = owner ? oob : sum_oob;
+                    acc = corr = oob = 0;
                     wp = 0;
                     pmask &= pmask - 1;
                     if (pmask) {
@@ -515,9 +508,16 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     // ---- phase C: lane finishes its own frame ----
     if (stream) {
         if (fi.work & 2) {
-            // udp_csum over [udp, udp + len16 (+1 odd)) relative to the udp start
+            // udp_csum sums LE words from the UDP start.  sum_t summed the words
+            // at even addresses: the same words when the UDP header starts at an
+            // even address; otherwise every word is byte-swapped, and the one's
+            // complement sum of swapped words is the swapped sum (the value
+            // mod 0xffff is all udp_csum_ok depends on; + 0xffff keeps the
+            // check subtraction from wrapping)
             const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
-            const uint32_t S = even ? sum_e + 256u * sum_o : sum_o + 256u * sum_e;
+            uint32_t f = (sum_t & 0xffffu) + (sum_t >> 16);
+            f = (f & 0xffffu) + (f >> 16);
+            const uint32_t S = even ? sum_t : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
             if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
                 r.status = DQDK_RX_INVALID_UDP_CSUM;
         }
@@ -565,20 +565,9 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
 
-    // Waves take 64-frame tiles from the batch's dispenser until it is
-    // exhausted; the grid is what fits on the GPU at once, so there is no
-    // second round of blocks and the load balances itself.
-    (void)wave;
     const uint32_t ntiles = (a.n + 63) / 64;
-    for (;;) {
-        unsigned long long g = 0;
-        if (lane == 0)
-            g = atomicAdd(a.tile_ctr, 1ull);
-        const uint64_t t = ((uint64_t)rfl((uint32_t)(g >> 32)) << 32) | rfl((uint32_t)g);
-        if (t >= ntiles)
-            break;
-        decode_wave_tile(a, (uint32_t)t, lane, lds_cnt1);
-    }
+    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves)
+        decode_wave_tile(a, t, lane, lds_cnt1);
 
     if (a.cnt1) {
         __syncthreads();

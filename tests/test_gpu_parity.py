@@ -297,3 +297,25 @@ def test_full_size_properties(L, stride, payloadsz):
     perm = rng.permutation(n)
     _, _, _, hist2, _ = run_gpu(umem, desc[perm], cfg, keys=False, histogram=True)
     assert np.array_equal(hist, hist2)
+
+
+@pytest.mark.parametrize("hpath,kernels", [
+    (D.F_HISTO_ATOMIC, {"rx_decode", "rx_abort", "rx_count", "rx_histo_atomic"}),
+    (D.F_HISTO_PARTITIONED, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_hist_prep", "rx_part2",
+                             "rx_slice_histo"})], ids=["atomic", "partitioned"])
+def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels):
+    _need_gpu()
+    umem, desc = D.synth_umem(1024, 1500, 4096)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | hpath)
+    q = D.RxQueue(0, cfg, len(desc))
+    try:
+        q.enable_timing(True)
+        for _ in range(3):
+            run_gpu(umem, desc, cfg, q=q)
+        t = q.read_timing()
+        assert {k for k, v in t.items() if v["launches"]} == kernels
+        for k in kernels:
+            assert t[k]["launches"] == 3 and t[k]["ms"] > 0
+        assert all(v["launches"] == 0 for v in q.read_timing().values())  # read clears
+    finally:
+        q.close()
