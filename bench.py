@@ -152,8 +152,9 @@ def main():
         "rx_part1": 8 * n + 8 * K,
         "rx_hist_prep": 0,
         "rx_part2": 6 * K + runs,
-        # u16 keys + runs read, one read-modify-write sweep of every touched 64 KB slice
-        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 16),
+        # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
+        # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
+        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14),
     }
     st = {}
     for name, s in stages.items():

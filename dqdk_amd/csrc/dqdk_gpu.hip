@@ -82,7 +82,9 @@ struct dqdk_gpu_queue {
     int cu_count = 256;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    uint32_t* d_hist = nullptr;
+    uint32_t* d_hist = nullptr;    // table base plane (u32/bin); value = d_hist + d_lo
+    uint8_t* d_lo = nullptr;       // table low-byte plane (partitioned sweep)
+    uint32_t* d_snap = nullptr;    // u32 snapshot for histogram_device_ptr (lazy)
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
     uint32_t* d_keys = nullptr;
@@ -216,6 +218,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.flags = q->cfg.flags;
         ha.batch_scratch = q->d_batch;
         ha.hist = q->d_hist;
+        ha.lo = q->d_lo;
         ha.scratch = q->d_hscratch;
         ha.part1 = q->d_part1;
         ha.part2 = q->d_part2;
@@ -249,6 +252,43 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         HIPCHK(hipGetLastError());
     }
     return 0;
+}
+
+// u32 view of table bins [first, first + nbins) (multiples of 16) into d_out, async.
+int combine(dqdk_gpu_queue* q, uint32_t* d_out, uint64_t first, uint64_t nbins)
+{
+    const uint64_t i0 = first / 16, i1 = (first + nbins) / 16;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((i1 - i0 + 255) / 256, (uint64_t)q->cu_count * 8u);
+    hipLaunchKernelGGL(hist_combine_kernel, dim3(grid), dim3(256), 0, q->stream, q->d_hist, q->d_lo, i0, i1, d_out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// Stream the u32 table view to the host in 64M-bin chunks: fn(host chunk, first bin, bins).
+template <typename F>
+int stream_table(dqdk_gpu_queue* q, F fn)
+{
+    const uint64_t chunk = 64ull << 20;
+    uint32_t* d_stage = nullptr;
+    uint32_t* h_stage = nullptr;
+    hipError_t e = hipMalloc(&d_stage, chunk * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipHostMalloc(&h_stage, chunk * sizeof(uint32_t), hipHostMallocDefault);
+    int rc = e == hipSuccess ? 0 : fail("histogram staging", e);
+    for (uint64_t o = 0; rc == 0 && o < DQDK_TRISTAN_HISTO_ENTRIES; o += chunk) {
+        const uint64_t m = std::min<uint64_t>(chunk, DQDK_TRISTAN_HISTO_ENTRIES - o);
+        rc = combine(q, d_stage, o, m);
+        if (rc == 0 && (e = hipMemcpyAsync(h_stage, d_stage, m * sizeof(uint32_t), hipMemcpyDeviceToHost, q->stream)) != hipSuccess)
+            rc = fail("hipMemcpyAsync", e);
+        if (rc == 0 && (e = hipStreamSynchronize(q->stream)) != hipSuccess)
+            rc = fail("hipStreamSynchronize", e);
+        if (rc == 0)
+            fn(h_stage, o, m);
+    }
+    (void)hipFree(d_stage);
+    if (h_stage)
+        (void)hipHostFree(h_stage);
+    return rc;
 }
 
 // Enqueue the raw payload gather of the batch just launched on q->stream;
@@ -393,9 +433,11 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));
     if (q->histo) {
-        if ((e = hipMalloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
+        if ((e = hipMalloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
             return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
-        if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess)
+        if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMemset(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
@@ -427,6 +469,8 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     for (auto ev : q->ev_free)
         (void)hipEventDestroy(ev);
     (void)hipFree(q->d_hist);
+    (void)hipFree(q->d_lo);
+    (void)hipFree(q->d_snap);
     (void)hipFree(q->d_cum);
     (void)hipFree(q->d_batch);
     (void)hipFree(q->d_keys);
@@ -585,9 +629,9 @@ int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_get: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
-    HIPCHK(hipStreamSynchronize(q->stream));
-    HIPCHK(hipMemcpy(host_hist, q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    return 0;
+    return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
+        memcpy(host_hist + o, h, m * sizeof(uint32_t));
+    });
 }
 
 int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist)
@@ -597,16 +641,10 @@ int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_accumulate: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
-    HIPCHK(hipStreamSynchronize(q->stream));
-    const size_t chunk = 64u << 20;  // entries per staging copy
-    std::vector<uint32_t> stage(chunk);
-    for (uint64_t o = 0; o < DQDK_TRISTAN_HISTO_ENTRIES; o += chunk) {
-        const size_t m = (size_t)std::min<uint64_t>(chunk, DQDK_TRISTAN_HISTO_ENTRIES - o);
-        HIPCHK(hipMemcpy(stage.data(), q->d_hist + o, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        for (size_t k = 0; k < m; k++)
-            host_hist[o + k] += stage[k];  // u32 wrap, like the shared atomic table
-    }
-    return 0;
+    return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
+        for (uint64_t k = 0; k < m; k++)
+            host_hist[o + k] += h[k];  // u32 wrap, like the shared atomic table
+    });
 }
 
 int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q)
@@ -617,10 +655,24 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q)
         return 0;
     HIPCHK(hipSetDevice(q->device));
     HIPCHK(hipMemsetAsync(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->stream));
+    HIPCHK(hipMemsetAsync(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES, q->stream));
     return 0;
 }
 
-uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q) { return q ? q->d_hist : nullptr; }
+uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q)
+{
+    if (!q || !q->d_hist)
+        return nullptr;
+    if (hipSetDevice(q->device) != hipSuccess)
+        return nullptr;
+    if (!q->d_snap && hipMalloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t)) != hipSuccess) {
+        q->d_snap = nullptr;
+        return nullptr;
+    }
+    if (combine(q, q->d_snap, 0, DQDK_TRISTAN_HISTO_ENTRIES) != 0 || hipStreamSynchronize(q->stream) != hipSuccess)
+        return nullptr;
+    return q->d_snap;
+}
 
 int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on)
 {
@@ -691,9 +743,7 @@ int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_copy: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
-    HIPCHK(hipMemcpyAsync(d_dst, q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                          q->stream));
-    return 0;
+    return combine(q, d_dst, 0, DQDK_TRISTAN_HISTO_ENTRIES);
 }
 
 int dqdk_gpu_histogram_add(dqdk_gpu_queue_t* q, const uint32_t* d_src)
@@ -721,7 +771,7 @@ int dqdk_gpu_histogram_nonzero(dqdk_gpu_queue_t* q, uint64_t* count)
     hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), q->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(hist_nonzero_kernel, dim3((uint32_t)q->cu_count * 8u), dim3(256), 0, q->stream, q->d_hist,
-                           DQDK_TRISTAN_HISTO_ENTRIES / 4, d);
+                           q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES / 16, d);
         e = hipGetLastError();
     }
     unsigned long long h = 0;
@@ -798,9 +848,10 @@ int dqdk_gpu_histogram_write_csv(dqdk_gpu_queue_t* q, int fd, uint64_t* bytes_wr
     auto format = [&](uint64_t c, int b) -> hipError_t {
         const uint64_t base = c * kCsvChunkBins, end = std::min(N, base + kCsvChunkBins);
         const uint32_t nblk = (uint32_t)((end - base + kCsvBinsPerBlock - 1) / kCsvBinsPerBlock);
-        hipLaunchKernelGGL(csv_len_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, base, end, d_blk[b]);
+        hipLaunchKernelGGL(csv_len_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, q->d_lo, base, end,
+                           d_blk[b]);
         hipLaunchKernelGGL(csv_scan_kernel, dim3(1), dim3(1024), 0, q->stream, d_blk[b], nblk);
-        hipLaunchKernelGGL(csv_write_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, base, end, d_blk[b],
+        hipLaunchKernelGGL(csv_write_kernel, dim3(nblk), dim3(kCsvThreads), 0, q->stream, q->d_hist, q->d_lo, base, end, d_blk[b],
                            d_txt[b]);
         hipError_t r = hipGetLastError();
         if (r == hipSuccess)

@@ -14,9 +14,11 @@ constexpr uint64_t kCsvChunkBins = 1ull << 22;                // 4M bins (16 MB 
 constexpr uint32_t kCsvChunkBlocks = (uint32_t)(kCsvChunkBins / kCsvBinsPerBlock);  // 1024
 constexpr uint64_t kCsvMaxLine = 4 + 1 + 1 + 1 + 5 + 1 + 10 + 1;  // "1511,5,65535,4294967295\n"
 
-__global__ void csv_len_kernel(const uint32_t* hist, uint64_t base, uint64_t end, uint64_t* blk_chars);
+// The table is value = hist[bin] + lo[bin] (rx_kernels.h): every reader takes both planes.
+__global__ void csv_len_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t base, uint64_t end, uint64_t* blk_chars);
 __global__ void csv_scan_kernel(uint64_t* blk_chars, uint32_t nblk);
-__global__ void csv_write_kernel(const uint32_t* hist, uint64_t base, uint64_t end, const uint64_t* blk_off, char* out);
+__global__ void csv_write_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t base, uint64_t end, const uint64_t* blk_off,
+                                 char* out);
 // Raw payload stream (tristan_process write(), src/tristan.c:318-324)
 constexpr int kRawThreads = 256;  // frames per block in the scan passes
 struct RawArgs {
@@ -35,6 +37,7 @@ __global__ void raw_len_kernel(RawArgs a);
 __global__ void raw_copy_kernel(RawArgs a);
 
 __global__ void hist_add_kernel(uint32_t* dst, const uint32_t* src, uint64_t n16);
-__global__ void hist_nonzero_kernel(const uint32_t* hist, uint64_t n16, unsigned long long* count);
+__global__ void hist_nonzero_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t n16, unsigned long long* count);
+__global__ void hist_combine_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t i0, uint64_t i1, uint32_t* out);
 
 }  // namespace dqdk

@@ -52,7 +52,10 @@ __device__ __forceinline__ char* put_u32(char* p, uint32_t v)
     return p + n;
 }
 
-__device__ __forceinline__ void load_row(const uint32_t* hist, uint64_t first, uint64_t end, uint32_t v[kCsvBinsPerThread])
+// Bin values [first, first + 16) of the table (value = base + low byte;
+// first is a multiple of 16).
+__device__ __forceinline__ void load_row(const uint32_t* hist, const uint8_t* lo, uint64_t first, uint64_t end,
+                                         uint32_t v[kCsvBinsPerThread])
 {
     if (first + kCsvBinsPerThread <= end) {
         const uint4* p = (const uint4*)(hist + first);
@@ -64,10 +67,15 @@ __device__ __forceinline__ void load_row(const uint32_t* hist, uint64_t first, u
             v[4 * j + 2] = x.z;
             v[4 * j + 3] = x.w;
         }
+        const uint4 b = ld_nt16((const uint4*)(lo + first));
+        const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < kCsvBinsPerThread; j++)
+            v[j] += (bw[j >> 2] >> (8 * (j & 3))) & 0xffu;
     } else {
 #pragma unroll
         for (int j = 0; j < kCsvBinsPerThread; j++)
-            v[j] = first + j < end ? hist[first + j] : 0u;
+            v[j] = first + j < end ? hist[first + j] + lo[first + j] : 0u;
     }
 }
 
@@ -97,7 +105,8 @@ __device__ __forceinline__ T block_excl_scan(T x, T* lds_wave, T* total)
 
 }  // namespace
 
-__global__ __launch_bounds__(kCsvThreads) void csv_len_kernel(const uint32_t* __restrict__ hist, uint64_t base, uint64_t end,
+__global__ __launch_bounds__(kCsvThreads) void csv_len_kernel(const uint32_t* __restrict__ hist,
+                                                             const uint8_t* __restrict__ lo, uint64_t base, uint64_t end,
                                                              uint64_t* __restrict__ blk_chars)
 {
     __shared__ uint64_t lds[kCsvThreads / 64];
@@ -105,7 +114,7 @@ __global__ __launch_bounds__(kCsvThreads) void csv_len_kernel(const uint32_t* __
     uint32_t v[kCsvBinsPerThread];
     uint64_t chars = 0;
     if (first < end) {
-        load_row(hist, first, end, v);
+        load_row(hist, lo, first, end, v);
 #pragma unroll
         for (int j = 0; j < kCsvBinsPerThread; j++)
             chars += v[j] ? line_len(first + j, v[j]) : 0u;
@@ -135,7 +144,8 @@ __global__ __launch_bounds__(1024) void csv_scan_kernel(uint64_t* __restrict__ b
         blk_chars[nblk] = carry;
 }
 
-__global__ __launch_bounds__(kCsvThreads) void csv_write_kernel(const uint32_t* __restrict__ hist, uint64_t base, uint64_t end,
+__global__ __launch_bounds__(kCsvThreads) void csv_write_kernel(const uint32_t* __restrict__ hist,
+                                                               const uint8_t* __restrict__ lo, uint64_t base, uint64_t end,
                                                                const uint64_t* __restrict__ blk_off, char* __restrict__ out)
 {
     __shared__ uint64_t lds[kCsvThreads / 64];
@@ -143,7 +153,7 @@ __global__ __launch_bounds__(kCsvThreads) void csv_write_kernel(const uint32_t* 
     uint32_t v[kCsvBinsPerThread];
     uint64_t chars = 0;
     if (first < end) {
-        load_row(hist, first, end, v);
+        load_row(hist, lo, first, end, v);
 #pragma unroll
         for (int j = 0; j < kCsvBinsPerThread; j++)
             chars += v[j] ? line_len(first + j, v[j]) : 0u;
@@ -280,20 +290,38 @@ __global__ __launch_bounds__(256) void hist_add_kernel(uint32_t* __restrict__ ds
     }
 }
 
-__global__ __launch_bounds__(256) void hist_nonzero_kernel(const uint32_t* __restrict__ hist, uint64_t n16,
-                                                          unsigned long long* __restrict__ count)
+__global__ __launch_bounds__(256) void hist_nonzero_kernel(const uint32_t* __restrict__ hist, const uint8_t* __restrict__ lo,
+                                                          uint64_t n16, unsigned long long* __restrict__ count)
 {
     __shared__ uint32_t lds[4];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t c = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
-        const uint4 a = ld_nt16((const uint4*)hist + i);
-        c += (a.x != 0) + (a.y != 0) + (a.z != 0) + (a.w != 0);
+        uint32_t v[16];
+        load_row(hist, lo, 16 * i, 16 * i + 16, v);
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            c += v[j] != 0u;
     }
     uint32_t total;
     (void)block_excl_scan<uint32_t>(c, lds, &total);
     if (threadIdx.x == 0 && total)
         atomicAdd(count, (unsigned long long)total);
+}
+
+// out[bin] = base[bin] + low[bin] for bins [16 * i0, 16 * i1) (the u32 table view).
+__global__ __launch_bounds__(256) void hist_combine_kernel(const uint32_t* __restrict__ hist, const uint8_t* __restrict__ lo,
+                                                          uint64_t i0, uint64_t i1, uint32_t* __restrict__ out)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += stride) {
+        uint32_t v[16];
+        load_row(hist, lo, 16 * i, 16 * i + 16, v);
+        uint4* o = (uint4*)(out + 16 * (i - i0));
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            o[j] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    }
 }
 
 }  // namespace dqdk

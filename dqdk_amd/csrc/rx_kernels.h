@@ -19,8 +19,10 @@
  *      rx_part2 (each 16K-key chunk of a bucket sorted by 16K-bin slice in
  *      LDS, written back as u16 slice-local keys + run offsets),
  *      rx_slice_histo (gathers the slice's runs, LDS histogram, one
- *      coalesced read-modify-write of the slice's 64 KB of table).  Same
- *      multiset of increments, so the table is bit-identical.
+ *      coalesced read-modify-write of the slice's 16 KB low-byte plane,
+ *      carries of 256 into the u32 base plane).  The table is held as
+ *      value = base[bin] + low[bin] (mod 2^32): the same values as the
+ *      reference's u32 table, with a 4x smaller per-batch sweep.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -85,7 +87,9 @@ struct HistoArgs {
     uint32_t E;
     uint32_t flags;
     const uint64_t* batch_scratch;
-    uint32_t* hist;
+    uint32_t* hist;     // table base plane (u32 per bin): the atomic path and carries add here
+    uint8_t* lo;        // table low-byte plane: the partitioned path's per-batch sweep
+                        // (bin value = hist[bin] + lo[bin], mod 2^32)
     uint32_t* scratch;  // kHistScratchWords
     uint32_t* part1;    // n*E keys grouped by bucket
     uint16_t* part2;    // n*E slice-local keys (key & 16383), each 16K chunk of a bucket sorted by slice

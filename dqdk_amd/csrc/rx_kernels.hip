@@ -895,15 +895,20 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     }
 }
 
-// Level 3: one block per 16K-bin slice: gather the slice's runs from every
-// chunk of its bucket into an LDS histogram, then one read-modify-write of
-// the slice's 64 KB of table (16 B per lane, coalesced, 8 in flight).
+// Level 3: one block per 16K-bin slice.  The run offsets of the bucket's
+// items (<= 512 at a time) are staged in LDS first, so gathering a run is
+// one dependent load, and each wave gathers two items at once; the slice's
+// 16 KB of the table's low-byte plane is loaded up front and read-modify-
+// written once after the LDS histogram is complete, with carries of 256
+// into the u32 base plane (rare: one per 256 increments of a bin).
 __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
+    __shared__ uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads];
     __shared__ uint32_t total;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
+    constexpr int kWavesS = kSliceThreads / 64;
     const uint32_t s = blockIdx.x;
     const uint32_t b = s / kSubs, sub = s % kSubs;
     const uint32_t i0 = a.scratch[kOffIstart + b], i1 = a.scratch[kOffIstart + b + 1];
@@ -916,43 +921,90 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
     for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
+    // events of this slice = sum of its run lengths; the first 512 items' runs stay in LDS
     uint32_t mine = 0;
-    constexpr int kG = 4;  // loads in flight per lane
-    for (uint32_t it = i0 + (uint32_t)wave; it < i1; it += kSliceThreads / 64) {
+    for (uint32_t it = i0 + (uint32_t)tid; it < i1; it += kSliceThreads) {
         const uint16_t* ro = a.runs + (uint64_t)it * kItemOffs + sub;
         const uint32_t lo = ro[0], hi = ro[1];
-        const uint16_t* src = a.part2 + bstart + (it - i0) * (uint32_t)kPartChunk;
-        for (uint32_t p0 = lo; p0 < hi; p0 += 64 * kG) {
-            uint32_t k[kG];
-#pragma unroll
-            for (int g = 0; g < kG; g++) {
-                const uint32_t p = p0 + 64 * g + lane;
-                k[g] = p < hi ? (uint32_t)src[p] : 0xffffffffu;
-            }
-#pragma unroll
-            for (int g = 0; g < kG; g++)
-                if (k[g] != 0xffffffffu)
-                    atomicAdd(&h[k[g]], 1u);
+        if (it < i0 + kSliceThreads) {
+            s_lo[tid] = lo;
+            s_hi[tid] = hi;
         }
         mine += hi - lo;
     }
-    if (lane == 0 && mine)
+    if (mine)
         atomicAdd(&total, mine);
     __syncthreads();
     if (total == 0)
         return;  // no events for this slice: table untouched
-    u32x4_t* g4 = (u32x4_t*)(a.hist + ((uint64_t)s << kSliceBits));
-    constexpr int kPer = (1 << kSliceBits) / 4 / kSliceThreads;  // 8 x 16 B per thread
-    u32x4_t v[kPer], g[kPer];
+    const uint64_t sb = (uint64_t)s << kSliceBits;
+    u32x4_t* lo4 = (u32x4_t*)(a.lo + sb);
+    constexpr int kLoPer = (1 << kSliceBits) / 16 / kSliceThreads;  // 2 x 16 B per thread
+    u32x4_t l[kLoPer];
 #pragma unroll
-    for (int k = 0; k < kPer; k++)
-        g[k] = g4[tid + k * kSliceThreads];
+    for (int j = 0; j < kLoPer; j++)
+        l[j] = lo4[tid + j * kSliceThreads];
+    constexpr int kG = 4;  // loads in flight per lane per item
+    for (uint32_t ib = i0; ib < i1; ib += kSliceThreads) {
+        const uint32_t nit = min(i1 - ib, (uint32_t)kSliceThreads);
+        if (ib != i0) {  // buckets with more than 512 items (skewed data)
+            __syncthreads();
+            if ((uint32_t)tid < nit) {
+                const uint16_t* ro = a.runs + (uint64_t)(ib + tid) * kItemOffs + sub;
+                s_lo[tid] = ro[0];
+                s_hi[tid] = ro[1];
+            }
+            __syncthreads();
+        }
+        for (uint32_t j = (uint32_t)wave; j < nit; j += 2 * kWavesS) {
+            const uint32_t j2 = j + kWavesS;
+            const uint32_t alo = s_lo[j], ahi = s_hi[j];
+            const uint32_t blo = j2 < nit ? s_lo[j2] : 0u, bhi = j2 < nit ? s_hi[j2] : 0u;
+            const uint16_t* asrc = a.part2 + bstart + (ib + j - i0) * (uint32_t)kPartChunk;
+            const uint16_t* bsrc = a.part2 + bstart + (ib + j2 - i0) * (uint32_t)kPartChunk;
+            const uint32_t steps = max(ahi - alo, bhi - blo);
+            for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kG) {
+                uint32_t ka[kG], kb[kG];
 #pragma unroll
-    for (int k = 0; k < kPer; k++)
-        v[k] = h4[tid + k * kSliceThreads];
+                for (int g = 0; g < kG; g++) {
+                    const uint32_t pa = alo + p0 + 64 * g + lane, pb = blo + p0 + 64 * g + lane;
+                    ka[g] = pa < ahi ? (uint32_t)asrc[pa] : 0xffffffffu;
+                    kb[g] = pb < bhi ? (uint32_t)bsrc[pb] : 0xffffffffu;
+                }
 #pragma unroll
-    for (int k = 0; k < kPer; k++)
-        g4[tid + k * kSliceThreads] = g[k] + v[k];  // u32 wrap, like the reference's atomic_fetch_add on u32
+                for (int g = 0; g < kG; g++) {
+                    if (ka[g] != 0xffffffffu)
+                        atomicAdd(&h[ka[g]], 1u);
+                    if (kb[g] != 0xffffffffu)
+                        atomicAdd(&h[kb[g]], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // low-byte plane: thread t owns bins [16t, 16t + 16) and [16(t + 512), +16)
+#pragma unroll
+    for (int j = 0; j < kLoPer; j++) {
+        const uint32_t b0 = 16u * (uint32_t)(tid + j * kSliceThreads);
+        const u32x4_t* hc = (const u32x4_t*)(h + b0);
+        uint32_t words[4] = {l[j].x, l[j].y, l[j].z, l[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32x4_t inc = hc[k];
+            const uint32_t incs[4] = {inc.x, inc.y, inc.z, inc.w};
+            uint32_t nw = 0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const uint32_t nv = ((words[k] >> (8 * m)) & 0xffu) + incs[m];
+                nw |= (nv & 0xffu) << (8 * m);
+                const uint32_t carry = nv & ~0xffu;
+                if (carry)
+                    a.hist[sb + b0 + 4 * k + m] += carry;  // u32 wrap, like the reference's atomic add
+            }
+            words[k] = nw;
+        }
+        lo4[tid + j * kSliceThreads] = u32x4_t{words[0], words[1], words[2], words[3]};
+    }
 }
 
 }  // namespace dqdk

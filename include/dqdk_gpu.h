@@ -182,14 +182,19 @@ int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist);
  * of per-GPU partials into the one tristan_histo_t (src/tristan.c:97). */
 int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist);
 int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
-/* Device pointer of the histogram (for RCCL reduce across GPUs), or NULL. */
+/* The device table is held as two planes (u32 base + low byte, value = sum
+ * mod 2^32; the partitioned path sweeps only the 0.6 GB low plane per
+ * batch).  device_ptr materialises the u32 table into a queue-owned device
+ * buffer (synchronous) and returns it, valid until the next call or queue
+ * destroy; NULL if the queue has no histogram. */
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
 
 /* ---- end-of-run egress (tristan_fini, src/tristan.c:162-233) ------------- */
 /* Merge helpers for per-GPU partial tables.  d_dst / d_src are device
  * pointers to DQDK_TRISTAN_HISTO_ENTRIES u32 (16-B aligned) reachable from
  * the queue's device; both run async on the queue stream.  copy: d_dst =
- * table (e.g. into an RCCL reduce buffer); add: table += d_src (u32 wrap). */
+ * the u32 table (e.g. into an RCCL reduce buffer); add: table += d_src (u32
+ * wrap). */
 int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst);
 int dqdk_gpu_histogram_add(dqdk_gpu_queue_t* q, const uint32_t* d_src);
 /* Number of non-zero bins (synchronous). */

@@ -319,3 +319,46 @@ def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels):
         assert all(v["launches"] == 0 for v in q.read_timing().values())  # read clears
     finally:
         q.close()
+
+
+def _peaked(n, first, rng):
+    """n clean 1500-B frames whose events pile onto 4 bins (counts >> 256)."""
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=False, first=first)
+    ev = umem.reshape(n, 4096)[:, 42:42 + 91 * 16].reshape(n, 91, 16)
+    peaks = [(3, 1, 0x12, 0x34), (700, 4, 0xff, 0xff), (1511, 5, 0, 0), (0, 0, 0, 0)]
+    pick = rng.integers(0, len(peaks) + 2, size=(n, 91))
+    for k, (chl, hc, e5, e6) in enumerate(peaks):
+        m = pick == k
+        ev[..., 2][m] = chl & 0xFF
+        ev[..., 3][m] = chl >> 8
+        ev[..., 5][m] = e5
+        ev[..., 6][m] = e6
+        ev[..., 8][m] = hc
+    return umem, desc
+
+
+def test_auto_path_mixes_atomic_and_partitioned_batches_with_carries():
+    """One queue, batches on both sides of the partition threshold: the atomic
+    path adds to the table's base plane, the partitioned sweep to its low-byte
+    plane with carries of 256; the table must equal the oracle's over all
+    batches (hot bins pass many multiples of 256 within and across batches)."""
+    _need_gpu()
+    rng = np.random.default_rng(11)
+    cfg = D.RxConfig(payloadsz=1458)  # auto path: partitioned at >= 4M events
+    keys_all = []
+    with D.RxQueue(0, cfg, 48000) as q:
+        first = 0
+        for n in (1024, 48000, 2048, 48000, 512):
+            umem, desc = _peaked(n, first, rng)
+            first += n
+            run_gpu(umem, desc, cfg, keys=False, q=q)
+            r, _, k = O.rx_batch(umem, desc, 1458)
+            kk = k.reshape(-1, 91)[r["status"] == 0].ravel()
+            keys_all.append(kk[kk != D.KEY_NONE])
+        hist = q.histogram()
+        assert q.histogram_nonzero() == int(np.count_nonzero(hist))
+    u, c = np.unique(np.concatenate(keys_all), return_counts=True)
+    assert c.max() > 100000
+    nz = np.flatnonzero(hist)
+    np.testing.assert_array_equal(nz, u)
+    np.testing.assert_array_equal(hist[nz], c)
