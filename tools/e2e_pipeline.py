@@ -19,6 +19,7 @@ device-resident by definition).
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import sys
 import time
@@ -39,6 +40,10 @@ def main():
     p.add_argument("--stride", type=int, default=0)
     p.add_argument("--records", action="store_true", help="also copy decoded records back")
     p.add_argument("--no-csum", action="store_true")
+    p.add_argument("--copy", choices=["image", "frames"], default="frames",
+                   help="H2D the whole UMEM image, or only the first frame_len bytes of each chunk "
+                        "(one strided hipMemcpy2DAsync; UMEM layout and descriptors unchanged)")
+    p.add_argument("--no-zero-copy", action="store_true")
     args = p.parse_args()
 
     import torch
@@ -59,6 +64,17 @@ def main():
         imgs.append(t)
         descs.append(torch.from_numpy(d.view(np.uint8)).pin_memory())
     umem_bytes = imgs[0].numel()
+
+    # strided copy: rows of `width` bytes at pitch `stride` (frames sit at addr = i * stride)
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy2DAsync.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                     C.c_int, C.c_void_p]
+    width = (L + 63) // 64 * 64
+    assert width <= stride
+
+    def h2d_frames(dst, src, stream):
+        rc = hip.hipMemcpy2DAsync(dst.data_ptr(), stride, src.data_ptr(), stride, width, n, 1, stream.cuda_stream)
+        assert rc == 0, f"hipMemcpy2DAsync failed: {rc}"
 
     q = D.RxQueue(0, cfg, n)
     s_h2d, s_rx, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
@@ -83,7 +99,10 @@ def main():
             with torch.cuda.stream(s_h2d):
                 if sl["used"]:
                     s_h2d.wait_event(sl["done"])  # kernels of batch b-depth finished reading the slot
-                sl["umem"].copy_(imgs[img], non_blocking=True)
+                if args.copy == "image":
+                    sl["umem"].copy_(imgs[img], non_blocking=True)
+                else:
+                    h2d_frames(sl["umem"], imgs[img], s_h2d)
                 sl["desc"].copy_(descs[img], non_blocking=True)
                 sl["copied"].record(s_h2d)
             s_rx.wait_event(sl["copied"])
@@ -113,10 +132,10 @@ def main():
         assert (r["status"] == D.RX_OK).all()
 
     pk = n * args.batches
-    h2d = (umem_bytes + n * 16) * args.batches
+    h2d = ((umem_bytes if args.copy == "image" else n * width) + n * 16) * args.batches
     d2h = (n * 8 + (n * E * 4 if args.records else 0)) * args.batches
     out = {
-        "pipeline": f"pinned H2D -> rx -> D2H, depth {args.depth}, {n} frames/batch",
+        "pipeline": f"pinned H2D ({args.copy}) -> rx -> D2H, depth {args.depth}, {n} frames/batch",
         "frame_len": L, "stride": stride, "batches": args.batches, "records_d2h": args.records,
         "csum": not args.no_csum,
         "Mpkt_s": round(pk / sec / 1e6, 3),
@@ -125,6 +144,10 @@ def main():
         "pcie_d2h_GB_s": round(d2h / sec / 1e9, 2),
     }
 
+    if args.no_zero_copy:
+        q.close()
+        print(json.dumps(out), flush=True)
+        return
     # zero-copy host drop-in (dqdk_gpu_rx_batch): kernels read the mapped UMEM over PCIe
     umem_np = imgs[0].numpy()
     desc_np = descs[0].numpy().view(D.DESC_DTYPE)
