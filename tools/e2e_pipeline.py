@@ -149,8 +149,9 @@ def main():
         print(json.dumps(out), flush=True)
         return
     # zero-copy host drop-in (dqdk_gpu_rx_batch): kernels read the mapped UMEM over PCIe
-    umem_np = imgs[0].numpy()
-    desc_np = descs[0].numpy().view(D.DESC_DTYPE)
+    # a fresh (pageable) image: hipHostRegister refuses memory torch has already pinned
+    del imgs, slots
+    umem_np, desc_np = D.synth_umem(n, L, stride, queue=0, threads=16)
     q.use_own_stream()
     q.register_umem(umem_np)
     q.process_batch(umem_np, desc_np)
