@@ -49,6 +49,8 @@ def parse_args():
     p.add_argument("--mode", default="energy-histo")
     p.add_argument("--no-csum", action="store_true", help="shipped path: checksum audit commented out")
     p.add_argument("--no-histo", action="store_true", help="decode only (no histogram accumulation)")
+    p.add_argument("--no-records", action="store_true",
+                   help="diagnostic: with --no-histo, pass no record buffer (decode writes nothing)")
     p.add_argument("--cpu-baseline-sec", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_summary.json"),
@@ -94,7 +96,8 @@ def main():
     q.set_stream(stream.cuda_stream)
 
     def step():
-        q.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(), d_keys.data_ptr())
+        q.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
+                         None if args.no_records else d_keys.data_ptr())
 
     for _ in range(args.warmup):
         step()
@@ -173,6 +176,22 @@ def main():
     LIB.check(LIB.lib().dqdk_gpu_membench_read(d_umem.data_ptr(), umem_bytes // 16 * 16, stream.cuda_stream, 5,
                                                C.byref(ms)), "membench_read")
     stream_gbs = umem_bytes // 16 * 16 / (ms.value * 1e-3) / 1e9
+    # the same frames read as rx_decode reads them (one wave per frame) and
+    # 4 B per event written: the pattern's practical rate without arithmetic
+    fbytes = (L + 15) // 16 * 16
+    pattern = {}
+    for name, flat, out in (("per_frame", 0, True), ("per_frame_read_only", 0, False), ("flat", 1, True),
+                            ("flat_read_only", 1, False)):
+        LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, fbytes, n,
+                                                     d_keys.data_ptr() if (E and out) else None, 4 * E if out else 0,
+                                                     flat, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
+        pattern[name] = round(n * (fbytes + (4 * E if out else 0)) / (ms.value * 1e-3) / 1e9, 1)
+    # contiguous 4:1 read:write copy over the same bytes (no frames): records buffer as the sink
+    mix_n = min(n, d_keys.numel() * 4 // stride)
+    LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, stride, mix_n, d_keys.data_ptr(), 0, 3,
+                                                 stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
+    pattern["contiguous_mix_4to1"] = round(mix_n * stride * 1.25 / (ms.value * 1e-3) / 1e9, 1)
+    pattern_gbs = pattern["per_frame"]
 
     hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo") if k in st]
     histogram = None
@@ -206,6 +225,8 @@ def main():
                 "alg_bytes_per_frame": 16 + L + 8 + 4 * E, "frames_per_launch": n,
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
+                "measured_frames_pattern_GB_s": pattern,
+                "frac_of_measured_pattern": round(dec["GB_s"] / pattern_gbs, 4) if dec else None,
                 "slowest_kernel": dom}
 
     # ---- CPU baseline: the oracle (C restatement) on rank 0 at N=1 ----------

@@ -183,7 +183,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
     const uint32_t nblk = (n + kTile - 1) / kTile;
-    const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * 8u);
+#ifndef DQDK_DEC_BLOCKS_PER_CU
+#define DQDK_DEC_BLOCKS_PER_CU 8u
+#endif
+    const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * DQDK_DEC_BLOCKS_PER_CU);
     {
         StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_decode_kernel, dim3(grid_dec), dim3(kTile), 0, q->stream, ra);

@@ -19,6 +19,68 @@ __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cas
 constexpr uint32_t kChannels = DQDK_TRISTAN_CHANNELS;
 constexpr uint32_t kHists = DQDK_TRISTAN_HISTS;
 
+// Streaming geometry of one frame, relative to a0 = frame address & ~15.
+// Chunk c covers bytes [16c + q4, 16c + q4 + 16): q4 puts event byte 2 of
+// every event at a fixed dword (offset r) of one chunk, so a lane decodes an
+// event from its own 16 B (no cross-lane shuffles).  Phase B streams chunks
+// [c_begin, c_begin + nch) as 2-KiB windows, 32 B (two chunks) per lane.
+struct Geo {
+    int q4, r;       // grid shift; byte offset of event byte 2 in its chunk
+    int c_begin;     // first streamed chunk
+    int nch;         // streamed chunks
+    int nwin;        // 2-KiB windows (128 chunks)
+    int de;          // chunk of event 0, relative to c_begin
+    int ct;          // last checksum chunk relative to c_begin (-1: no checksum bytes)
+    int keep;        // checksum bytes in chunk ct (1..16)
+    int cs_lo;       // checksum start (a0-relative): bytes [16 c_begin + q4, cs_lo) are the head correction
+};
+
+constexpr int kLaneBytes = 32;                    // two chunks per lane per window
+constexpr int kWinChunks = 64 * kLaneBytes / 16;  // 128
+constexpr uint32_t kWinBytes = 64u * kLaneBytes;  // 2 KiB
+
+__device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
+                                         uint32_t E)
+{
+    Geo g;
+    const bool dec = work & 1, cs = work & 2;
+    const int dec_lo = (int)(off0 + poff);
+    const int dec_hi = dec_lo + (int)(16 * E);
+    const int cs_lo = (int)(off0 + 14 + hs);
+    const int cs_hi = cs_lo + (int)len16 + (int)(len16 & 1);  // + the odd-length over-read byte
+    const int q = dec ? ((dec_lo + 2) & ~3) : 0;
+    g.q4 = q & 15;
+    g.r = (dec_lo + 2) & 3;
+    g.cs_lo = cs_lo;
+    int lo = 0x7fffffff, hi = 0;
+    if (dec) {
+        lo = dec_lo;
+        hi = dec_hi;
+    }
+    if (cs) {
+        lo = min(lo, cs_lo);
+        hi = max(hi, cs_hi);
+    }
+    if (hi <= lo) {
+        g.c_begin = g.nch = g.nwin = g.de = g.keep = 0;
+        g.ct = -1;
+        return g;
+    }
+    g.c_begin = (lo - g.q4) >> 4;  // lo >= 14 > q4
+    g.nch = ((hi - g.q4 + 15) >> 4) - g.c_begin;
+    g.nwin = (g.nch + kWinChunks - 1) / kWinChunks;
+    g.de = dec ? (q >> 4) - g.c_begin : 0;  // 0 or 1 (the chunk of event byte 2 is c_begin or the next)
+    if (cs && cs_hi > cs_lo) {
+        const int ct = (cs_hi - 1 - g.q4) >> 4;
+        g.ct = ct - g.c_begin;
+        g.keep = cs_hi - (16 * ct + g.q4);
+    } else {
+        g.ct = -1;
+        g.keep = 16;
+    }
+    return g;
+}
+
 // Per-frame hand-off from phase A (lane per frame) to phase B (wave per frame).
 struct FrameInfo {
     uint64_t addr;
@@ -28,55 +90,11 @@ struct FrameInfo {
     uint16_t check;    // udp->check as stored (LE u16)
     uint8_t status;
     uint8_t poff;      // payload offset from the frame start
-    uint8_t work;      // bit0 decode, bit1 udp checksum pending, 4 = KEY_NONE fill only
+    uint8_t work;      // bit0 decode, bit1 udp checksum pending
     uint8_t hs;        // ihl * 4
-};
-
-// Streaming geometry of one frame, relative to a0 = frame address & ~15.
-// Chunk c covers bytes [16c + q4, 16c + q4 + 16): q4 puts event byte 2 of
-// every event at a fixed dword (offset r) of one lane's chunk, so a lane
-// decodes its event from its own 16 B (no cross-lane shuffles).
-struct Geo {
-    int q4, r, ce0;         // grid shift, byte offset of event byte 2 in its dword, chunk of event 0
-    int c_begin, c_end;     // streamed chunks
-    int nwin;               // 1-KiB windows (64 chunks)
-    int ct;                 // last chunk holding checksum bytes (-1: none)
-    int cs_lo, cs_hi;       // checksum byte range [udp, udp + len16 (+1 odd))
-};
-
-__device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
-                                         uint32_t E)
-{
+    uint32_t head;     // checksum head correction: word sum of bytes [16 c_begin + q4, cs_lo)
     Geo g;
-    const bool dec = work & 1, cs = work & 2;
-    const int dec_lo = (int)(off0 + poff);
-    const int dec_hi = dec_lo + (int)(16 * E);
-    g.cs_lo = (int)(off0 + 14 + hs);
-    g.cs_hi = g.cs_lo + (int)len16 + (int)(len16 & 1);
-    const int q = dec ? ((dec_lo + 2) & ~3) : 0;
-    g.q4 = q & 15;
-    g.r = (dec_lo + 2) & 3;
-    g.ce0 = q >> 4;
-    int lo = 0x7fffffff, hi = 0;
-    if (dec) {
-        lo = dec_lo;
-        hi = dec_hi;
-    }
-    if (cs) {
-        lo = min(lo, g.cs_lo);
-        hi = max(hi, g.cs_hi);
-    }
-    if (hi <= lo) {
-        g.c_begin = g.c_end = g.nwin = 0;
-        g.ct = -1;
-        return g;
-    }
-    g.c_begin = (lo - g.q4) >> 4;  // lo >= 14 > q4
-    g.c_end = (hi - g.q4 + 15) >> 4;
-    g.nwin = (g.c_end - g.c_begin + 63) >> 6;
-    g.ct = (cs && g.cs_hi > g.cs_lo) ? ((g.cs_hi - 1 - g.q4) >> 4) : -1;
-    return g;
-}
+};
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int b) { return (w >> (8 * b)) & 0xffu; }
 
@@ -124,7 +142,11 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
 #pragma unroll
     for (int k = 0; k < 7; k++) {
         u32x4 v = {0u, 0u, 0u, 0u};
+#ifdef DQDK_DIAG_NOHDR  // timing diagnostic only: every lane parses frame 0's header line
+        uint64_t o = (a.desc[0].addr & ~15ull) + 16ull * k;
+#else
         uint64_t o = a0 + 16ull * k;
+#endif
         if (addr < a.umem_size && o + 16 <= a.umem_size)
             v = *(const u32x4*)(a.umem + o);
         w[4 * k + 0] = v.x;
@@ -155,6 +177,8 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
     fi.poff = 0;
     fi.work = 0;
     fi.hs = 0;
+    fi.head = 0;
+    fi.g = frame_geo(0, 0, 0, 0, 0, 0);
     needB = false;
 
     if (a.flags & DQDK_GPU_F_PREFILTER) {  // src/bpf/forwarder.bpf.c:38-96
@@ -257,6 +281,26 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
     if (datalen != 0 && a.E != 0)
         fi.work |= 1;
     needB = fi.work != 0;
+    if (needB) {
+        fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E);
+        if ((fi.work & 2) && fi.g.ct >= 0) {
+            // head correction: the first streamed chunk starts at G <= cs_lo
+            // (4-aligned, G > cs_lo - 16); its bytes before the UDP header are
+            // header bytes staged above (cs_lo <= 15 + 14 + 60 < 92)
+            const int G = 16 * fi.g.c_begin + fi.g.q4;
+            const int Lc = fi.g.cs_lo;
+            uint32_t head = 0;
+#pragma unroll
+            for (int k = 0; k < 23; k++) {
+                const int p = 4 * k;
+                uint32_t m = 0;
+                if (p >= G && p < Lc)
+                    m = (Lc - p >= 4) ? 0xffffffffu : ((1u << (8 * (Lc - p))) - 1u);
+                head = __builtin_amdgcn_udot2(as_u16x2(w[k] & m), u16x2{1, 1}, head, false);
+            }
+            fi.head = head;
+        }
+    }
 #undef FB
 }
 
@@ -277,19 +321,31 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 
 // ---------------------------------------------------------------------------
 // Each wave owns 64-frame tiles end to end (no block barriers):
-//   phase A  lane l parses frame 64*tile + l (headers staged in VGPRs);
-//   phase B  the wave streams the payloads of its frames that need it as
-//            ONE continuous sequence of 1-KiB windows (64 lanes x 16 B
-//            aligned buffer loads), kRing windows in flight across frame
-//            boundaries; per-frame parameters come from the owning lane
-//            (readlane) and per-frame partial sums go back to it (writelane);
+//   phase A  lane l parses frame 64*tile + l (headers staged in VGPRs) and
+//            prepares its frame's stream: SRD base/extent, window count,
+//            decode shift, checksum head correction;
+//   phase B  the wave streams the chunks of its frames as ONE sequence of
+//            2-KiB windows (lane = 32 B = two 16-B chunks), kRingW windows
+//            in flight across frame boundaries; each frame has its own SRD
+//            whose extent ends at the frame's last chunk, so loads past it
+//            return zeros (no per-lane bounds tests); per-frame parameters
+//            come from the owning lane (readlane), per-frame sums go back to it;
 //   phase C  lane l finishes its own frame: checksum verdict, result record
 //            (coalesced), KEY_NONE records for non-OK frames.
-// The phase-B loop body is straight-line in VMEM terms (one load and one key
-// store per window; inactive lanes use out-of-range buffer offsets) so hipcc
-// can count the ring with vmcnt(N) instead of draining it.
+// Every window issues exactly two loads and two key stores (lanes without an
+// event store to an out-of-range offset), so hipcc counts the ring with
+// vmcnt(N) on every path instead of draining it.
 // ---------------------------------------------------------------------------
-constexpr int kRing = 8;
+#ifndef DQDK_RINGW
+#define DQDK_RINGW 4
+#endif
+constexpr int kRingW = DQDK_RINGW;
+#ifndef DQDK_LD_AUX
+#define DQDK_LD_AUX 0
+#endif
+#ifndef DQDK_ST_AUX
+#define DQDK_ST_AUX 0
+#endif
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -318,206 +374,292 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
     return __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)nrec, 0x00020000);
 }
 
-// Per-lane (per-frame) streaming state kept in VGPRs of the owning lane.
+// LDS of one rx_decode block: partition bucket counts, per-frame out-of-bounds
+// counts and checksum sums (one slot per frame of each wave's tile), the
+// captured last checksum chunk of each frame, and a sink for lanes without
+// an event.  Frame slots are reset by their lane in phase C.
+constexpr int kLdsOob = 288;                      // [kWaves][64] out-of-bounds events per frame
+constexpr int kLdsSink = kLdsOob + kWaves * 64;   // lanes without an event count here
+constexpr int kLdsCnt = kLdsSink + 1;
+struct DecodeLds {
+    uint32_t cnt[kLdsCnt];       // [0, kL1Buckets): keys per L1 bucket (partitioned histogram)
+    uint32_t sum[kWaves * 64];   // checksum word sums per frame
+    u32x4 tail[kWaves * 64];     // last checksum chunk per frame (tail correction)
+};
+
+// Per-frame stream parameters in the owning lane's VGPRs.
+//   pk1 = nwin | de << 16 | r << 18 | dec << 20 | lw << 21 | th << 22 | tl << 23
+//   pk2 = tw | mw << 16
+// nwin: 2-KiB windows; de: chunk of event 0; r: event shift; dec: decode;
+// lw: some window needs per-lane checksum weights (chunks past ct), the
+// first such window is mw; tw/tl/th: window/lane/half holding the last
+// checksum chunk when it needs a tail correction (tw = 0xffff: none).
 struct LaneFrame {
-    uint32_t addr_lo, addr_hi;
-    uint32_t work;       // bit0 decode, bit1 checksum
-    Geo g;
+    uint32_t base_lo, base_hi;  // umem + a0 + 16 c_begin + q4
+    uint32_t nrec;              // streamed bytes inside the UMEM
+    uint32_t pk1, pk2;
+    int ct;
 };
 
-// Wave-uniform view of one frame (read from its owning lane).
-struct WaveFrame {
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t work;
-    int q4, r, ce0, c_begin, c_end, nwin, ct, cs_lo, cs_hi;
-};
+constexpr uint32_t kNoWin = 0xffffu;
 
-__device__ __forceinline__ void wave_frame(const RxArgs& a, const LaneFrame& lf, uint32_t lane_j, bool need_rsrc,
-                                           WaveFrame& W)
+__device__ __forceinline__ uint32_t pk_nwin(uint32_t pk1) { return pk1 & 0xffffu; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const LaneFrame& lf, uint32_t j)
 {
-    W.work = rdl(lf.work, lane_j);
-    W.q4 = (int)rdl((uint32_t)lf.g.q4, lane_j);
-    W.c_begin = (int)rdl((uint32_t)lf.g.c_begin, lane_j);
-    W.c_end = (int)rdl((uint32_t)lf.g.c_end, lane_j);
-    W.nwin = (int)rdl((uint32_t)lf.g.nwin, lane_j);
-    if (need_rsrc) {
-        const uint64_t addr = (uint64_t)rdl(lf.addr_lo, lane_j) | ((uint64_t)rdl(lf.addr_hi, lane_j) << 32);
-        const uint64_t a0 = addr & ~15ull;
-        W.rsrc = uniform_rsrc(a.umem + a0, a.umem_size > a0 ? a.umem_size - a0 : 0);
+    const uint64_t b = (uint64_t)rdl(lf.base_lo, j) | ((uint64_t)rdl(lf.base_hi, j) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, (int)rdl(lf.nrec, j), 0x00020000);
+}
+
+// Wave-uniform view of the frame being processed.
+struct PFrame {
+    uint32_t nwin, de, r, Ef, lw, th, tl, tw, mw;  // Ef = events to decode (0: frame not decoded)
+    int ct;
+};
+
+__device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uint32_t j, PFrame& P)
+{
+    const uint32_t pk1 = rdl(lf.pk1, j), pk2 = rdl(lf.pk2, j);
+    P.nwin = pk1 & 0xffffu;
+    P.de = (pk1 >> 16) & 3u;
+    P.r = (pk1 >> 18) & 3u;
+    P.Ef = (pk1 & (1u << 20)) ? a.E : 0u;
+    P.lw = (pk1 >> 21) & 1u;
+    P.th = (pk1 >> 22) & 1u;
+    P.tl = pk1 >> 23;
+    P.tw = pk2 & 0xffffu;
+    P.mw = pk2 >> 16;
+    P.ct = P.lw ? (int)rdl((uint32_t)lf.ct, j) : 0;
+}
+
+__device__ __forceinline__ void lds_add_u32(uint32_t lds_addr, uint32_t v)
+{
+    asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+}
+
+// One event per 16-B chunk v (event byte 2 at byte r of v.x): key record
+// store, then one LDS count: the key's L1 bucket, the frame's OOB slot for
+// an out-of-bounds event, the sink for a lane without an event.
+__device__ __forceinline__ void decode_chunk(const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef, uint32_t kbase,
+                                             uint32_t oob_slot, __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t* cnt)
+{
+    const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
+    const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
+    const uint32_t ch = x & 0xffffu;
+    const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
+    const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
+    uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
+    key = ch < kChannels ? key : DQDK_KEY_NONE;
+    key = hc < kHists ? key : DQDK_KEY_NONE;
+    const bool has = e < Ef;
+    __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has ? kbase + 4u * e : kOOB, 0, DQDK_ST_AUX);
+    // KEY_NONE >> kL1Shift = 2047 > oob_slot > every bucket
+    const uint32_t idx = has ? min(key >> kL1Shift, oob_slot) : (uint32_t)kLdsSink;
+#ifndef DQDK_DIAG_NOLDS  // timing diagnostic only
+    atomicAdd(&cnt[idx], 1u);
+#endif
+}
+
+// T = sum of the LE 16-bit words at even addresses of a chunk (chunk starts
+// are 4-aligned, so a dword's two halves)
+__device__ __forceinline__ uint32_t csum_chunk(const u32x4& v, u16x2 wt, uint32_t acc)
+{
+    acc = __builtin_amdgcn_udot2(as_u16x2(v.x), wt, acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(v.y), wt, acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(v.z), wt, acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(v.w), wt, acc, false);
+    return acc;
+}
+
+// both chunks of a lane interleaved: two independent dot2 chains
+__device__ __forceinline__ void csum_pair(const u32x4& v0, const u32x4& v1, u16x2 w0, u16x2 w1, uint32_t& acc0,
+                                          uint32_t& acc1)
+{
+    acc0 = __builtin_amdgcn_udot2(as_u16x2(v0.x), w0, acc0, false);
+    acc1 = __builtin_amdgcn_udot2(as_u16x2(v1.x), w1, acc1, false);
+    acc0 = __builtin_amdgcn_udot2(as_u16x2(v0.y), w0, acc0, false);
+    acc1 = __builtin_amdgcn_udot2(as_u16x2(v1.y), w1, acc1, false);
+    acc0 = __builtin_amdgcn_udot2(as_u16x2(v0.z), w0, acc0, false);
+    acc1 = __builtin_amdgcn_udot2(as_u16x2(v1.z), w1, acc1, false);
+    acc0 = __builtin_amdgcn_udot2(as_u16x2(v0.w), w0, acc0, false);
+    acc1 = __builtin_amdgcn_udot2(as_u16x2(v1.w), w1, acc1, false);
+}
+
+// Window wp of frame P (owned by lane `slot`): lane l holds chunks
+// 128 wp + l (v0) and 128 wp + 64 + l (v1), so each load, store and sum is
+// one contiguous 1-KiB span.  Chunks past the frame's extent read zeros.
+__device__ __forceinline__ void process_window(const RxArgs& a, const PFrame& P, uint32_t slot, uint32_t wslot0,
+                                               uint32_t wp, const u32x4& v0, const u32x4& v1, int lane, bool active,
+                                               __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc0, uint32_t& acc1,
+                                               DecodeLds& lds)
+{
+    const uint32_t jw = (uint32_t)kWinChunks * wp;
+    if (active && wp >= P.mw) {
+        // rare: E*16 reaches past the datagram, chunks past ct carry no checksum bytes
+        const int j0 = (int)jw + lane;
+        csum_pair(v0, v1, j0 <= P.ct ? u16x2{1, 1} : u16x2{0, 0}, j0 + 64 <= P.ct ? u16x2{1, 1} : u16x2{0, 0}, acc0,
+                  acc1);
     } else {
-        W.r = (int)rdl((uint32_t)lf.g.r, lane_j);
-        W.ce0 = (int)rdl((uint32_t)lf.g.ce0, lane_j);
-        W.ct = (int)rdl((uint32_t)lf.g.ct, lane_j);
-        W.cs_lo = (int)rdl((uint32_t)lf.g.cs_lo, lane_j);
-        W.cs_hi = (int)rdl((uint32_t)lf.g.cs_hi, lane_j);
+        // (inactive windows read zeros; sums of frames without a checksum are ignored)
+        csum_pair(v0, v1, u16x2{1, 1}, u16x2{1, 1}, acc0, acc1);
     }
+    if (active && wp == P.tw) {  // the last checksum chunk, for phase C's tail correction
+        if (lane == (int)P.tl)
+            lds.tail[wslot0 + slot] = P.th ? v1 : v0;
+    }
+    // records of this wave tile live at keys_rsrc + (slot*E + e)*4
+    const uint32_t Ef = active ? P.Ef : 0u;
+    const uint32_t e0 = jw + (uint32_t)lane - P.de;
+    const uint32_t kbase = slot * a.E * 4u;
+    const uint32_t oob_slot = (uint32_t)kLdsOob + wslot0 + slot;
+    decode_chunk(v0, P.r, e0, Ef, kbase, oob_slot, keys_rsrc, lds.cnt);
+    decode_chunk(v1, P.r, e0 + 64u, Ef, kbase, oob_slot, keys_rsrc, lds.cnt);
 }
 
-// One 1-KiB window of frame P (owned by lane `slot`): checksum sums + decode
-// of the events whose byte 2 falls in each lane's chunk.
-__device__ __forceinline__ void process_window(const RxArgs& a, const WaveFrame& P, uint32_t slot, int w,
-                                               const u32x4& v, int lane, bool active,
-                                               __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t& acc, uint32_t& corr,
-                                               uint32_t& oob, uint32_t* lds_cnt1)
-{
-    const int c0 = P.c_begin + 64 * w;
-    const int c = c0 + lane;
-    const bool inr = active && c < P.c_end;
-    if (P.work & 2) {
-        // T = sum of the LE 16-bit words at even addresses (chunk starts are
-        // 4-aligned, so a dword's two halves): one dot2 per dword; lanes
-        // outside the checksum range get zero weights
-        const bool incs = inr && c <= P.ct;
-        const u16x2 wt = incs ? u16x2{1, 1} : u16x2{0, 0};
-        acc = __builtin_amdgcn_udot2(as_u16x2(v.x), wt, acc, false);
-        acc = __builtin_amdgcn_udot2(as_u16x2(v.y), wt, acc, false);
-        acc = __builtin_amdgcn_udot2(as_u16x2(v.z), wt, acc, false);
-        acc = __builtin_amdgcn_udot2(as_u16x2(v.w), wt, acc, false);
-        if (active) {
-            // uniform: the first checksum chunk (lane 0 of window 0) and the
-            // last one (chunk ct) may hold bytes outside [cs_lo, cs_hi)
-            // (cs_hi includes the odd-length over-read byte); their sums are
-            // taken from the owning lane's data in SGPRs and subtracted from
-            // the frame total at its end
-            if (w == 0 && P.ct >= P.c_begin) {  // (ct < c_begin: no checksum bytes at all)
-                const int nb = P.cs_lo - (16 * P.c_begin + P.q4);
-                if (nb > 0) {
-                    uint32_t de, dd;
-                    chunk_range_sums(rdl(v.x, 0), rdl(v.y, 0), rdl(v.z, 0), rdl(v.w, 0), 0, nb, de, dd);
-                    corr += de + 256u * dd;
-                }
-            }
-            const int lt = P.ct - c0;
-            if (lt >= 0 && lt < 64) {
-                const int keep = P.cs_hi - (16 * P.ct + P.q4);
-                if (keep < 16) {
-                    const uint32_t l = (uint32_t)lt;
-                    uint32_t de, dd;
-                    chunk_range_sums(rdl(v.x, l), rdl(v.y, l), rdl(v.z, l), rdl(v.w, l), keep, 16, de, dd);
-                    corr += de + 256u * dd;
-                }
-            }
-        }
-    }
-    if (P.work & 1) {
-        const uint32_t e = (uint32_t)(c - P.ce0);
-        const bool has_evt = inr && e < a.E;
-        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, P.r);  // event bytes 2..5
-        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, P.r);  // event bytes 6..9
-        const uint32_t ch = x & 0xffffu;
-        const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
-        const uint32_t hc = (y >> 16) & 7u;                                // hist_class:3
-        const bool bad = ch >= kChannels || hc >= kHists;
-        const uint32_t key = bad ? DQDK_KEY_NONE : ((ch * kHists + hc) << 16) | bin;
-        // records of this wave tile live at keys_rsrc + (slot*E + e)*4; one store per window
-        __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has_evt ? (slot * a.E + e) * 4u : kOOB, 0, 0);
-        if (a.cnt1)  // capacity of the key's L1 bucket (slot kL1Buckets absorbs the rest)
-            atomicAdd(&lds_cnt1[has_evt && !bad ? (key >> kL1Shift) : (uint32_t)kL1Buckets], 1u);
-        oob += (uint32_t)__builtin_popcountll(__ballot(has_evt && bad));  // wave-uniform
-    }
-}
-
-__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t* lds_cnt1)
+__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t wave,
+                                                 DecodeLds& lds)
 {
     const uint32_t i = tile * 64 + lane;
     const bool live = i < a.n;
+    const uint32_t wslot0 = wave * 64;
 
     // ---- phase A: lane parses frame i ----
     FrameInfo fi;
     dqdk_gpu_rx_result_t r;
     bool needB = false;
-    LaneFrame lf;
     if (live)
         parse_frame(a, i, fi, r, needB);
     bool stream = false;
+    LaneFrame lf;
+    lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
+    lf.pk2 = kNoWin | (kNoWin << 16);
+    lf.ct = -1;
     if (needB) {
-        lf.g = frame_geo(fi.work, (uint32_t)(fi.addr & 15), fi.poff, fi.hs, fi.len16, a.E);
-        stream = lf.g.nwin > 0;
+        const Geo& g = fi.g;
+        stream = g.nwin > 0;
         if (!stream && !udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))  // empty datagram checksum
             r.status = DQDK_RX_INVALID_UDP_CSUM;
-    } else {
-        lf.g = frame_geo(0, 0, 0, 0, 0, 0);
+        const uint64_t boff = (fi.addr & ~15ull) + 16ull * (uint64_t)g.c_begin + (uint64_t)g.q4;
+        const uint64_t base = (uint64_t)a.umem + boff;
+        const uint64_t ext = 16ull * (uint64_t)g.nch;
+        const uint64_t room = a.umem_size > boff ? a.umem_size - boff : 0ull;
+        lf.base_lo = (uint32_t)base;
+        lf.base_hi = (uint32_t)(base >> 32);
+        lf.nrec = (uint32_t)(ext < room ? ext : room);
+        const bool cs = fi.work & 2;
+        const bool lw = cs && g.ct < g.nch - 1;   // chunks past ct are streamed (decode reaches further)
+        const bool tc = cs && g.ct >= 0 && g.keep < 16;
+        const uint32_t ct = (uint32_t)(g.ct < 0 ? 0 : g.ct);
+        lf.pk1 = ((uint32_t)g.nwin & 0xffffu) | (((uint32_t)g.de & 3u) << 16) | (((uint32_t)g.r & 3u) << 18) |
+                 ((fi.work & 1u) << 20) | ((lw ? 1u : 0u) << 21) | (((ct >> 6) & 1u) << 22) | ((ct & 63u) << 23);
+        const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
+        const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
+        lf.pk2 = tw | (mw << 16);
+        lf.ct = g.ct;
     }
-    lf.addr_lo = (uint32_t)fi.addr;
-    lf.addr_hi = (uint32_t)(fi.addr >> 32);
-    lf.work = stream ? fi.work : 0u;
+    if (!stream)
+        lf.pk1 = 0;
 
-    // ---- phase B: stream the payloads ----
-    uint32_t sum_t = 0, sum_oob = 0;  // this lane's frame, written by the owner loop
+    // ---- phase B: stream the frames ----
     const uint64_t smask0 = __ballot(stream);
     if (smask0) {
-        const int total = (int)wave_sum_dpp(stream ? (uint32_t)lf.g.nwin : 0u);
+        const int total = (int)wave_sum_dpp(pk_nwin(lf.pk1));
         const __amdgpu_buffer_rsrc_t keys_rsrc =
             uniform_rsrc(a.keys + (uint64_t)tile * 64 * a.E, a.keys ? (uint64_t)64 * a.E * 4u : 0u);
+        const uint32_t lane16 = (uint32_t)lane * 16u;
         // load cursor
         uint64_t lmask = smask0;
         uint32_t jl = (uint32_t)__builtin_ctzll(lmask);
-        int wl = 0;
-        WaveFrame L;
-        wave_frame(a, lf, jl, true, L);
-        auto issue = [&](u32x4& dst) {
-            const int c = L.c_begin + 64 * wl + lane;
-            const bool ok = lmask != 0 && c < L.c_end;
-            dst = __builtin_amdgcn_raw_buffer_load_b128(L.rsrc, ok ? (uint32_t)(16 * c + L.q4) : kOOB, 0, 0);
-            if (lmask != 0 && ++wl == L.nwin) {
+        uint32_t wl = 0, lnwin = pk_nwin(rdl(lf.pk1, jl));
+        __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
+        auto issue = [&](u32x4& d0, u32x4& d1) {
+            const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes : kOOB);
+            d0 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo, 0, DQDK_LD_AUX);
+            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u, 0, DQDK_LD_AUX);
+            if (lmask != 0 && ++wl == lnwin) {
                 wl = 0;
                 lmask &= lmask - 1;
                 if (lmask) {
                     jl = (uint32_t)__builtin_ctzll(lmask);
-                    wave_frame(a, lf, jl, true, L);
+                    lnwin = pk_nwin(rdl(lf.pk1, jl));
+                    lrs = frame_rsrc(lf, jl);
                 }
             }
         };
-        u32x4 buf[kRing];
+        u32x4 b0[kRingW], b1[kRingW];
 #pragma unroll
-        for (int d = 0; d < kRing; d++)
-            issue(buf[d]);
+        for (int d = 0; d < kRingW; d++) {
+            // two dropped stores per window, as in the loop body (store, store,
+            // load, load): the loop is entered with the same vmcnt pattern it
+            // repeats, so the wait for window d is vmcnt(4 * (kRingW - 1)), not
+            // the prologue's shorter count (distinct offsets: not merged)
+            __builtin_amdgcn_raw_buffer_store_b32(0u, keys_rsrc, kOOB + lane16 + 8u * d, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(0u, keys_rsrc, kOOB + lane16 + 8u * d + 4u, 0, 0);
+            issue(b0[d], b1[d]);
+        }
         // process cursor
         uint64_t pmask = smask0;
         uint32_t jp = (uint32_t)__builtin_ctzll(pmask);
-        int wp = 0;
-        WaveFrame P;
-        wave_frame(a, lf, jp, false, P);
-        uint32_t acc = 0, corr = 0, oob = 0;  // acc per lane; corr, oob wave-uniform
-        for (int k = 0; k < total; k += kRing) {
+        uint32_t wp = 0;
+        PFrame P;
+        pframe(a, lf, jp, P);
+        uint32_t acc0 = 0, acc1 = 0;
+        for (int k = 0; k < total; k += kRingW) {
 #pragma unroll
-            for (int d = 0; d < kRing; d++) {
+            for (int d = 0; d < kRingW; d++) {
                 const bool active = k + d < total;
-                process_window(a, P, jp, wp, buf[d], lane, active, keys_rsrc, acc, corr, oob, lds_cnt1);
+                process_window(a, P, jp, wslot0, wp, b0[d], b1[d], lane, active, keys_rsrc, acc0, acc1, lds);
                 if (active && ++wp == P.nwin) {
-                    // hand the frame's totals to its owning lane
-                    const bool owner = lane == (int)jp;
-                    if (P.work & 2) {
-                        const uint32_t t = wave_sum_dpp(acc) - corr;
-                        sum_t = owner ? t : sum_t;
-                    }
-                    sum_oob = owner ? oob : sum_oob;
-                    acc = corr = oob = 0;
+                    // the frame's checksum word sum to its LDS slot: every lane adds into
+                    // one address (inline asm: the compiler's atomic optimizer would turn
+                    // a uniform-address atomicAdd into a 64-step readlane loop)
+#ifndef DQDK_DIAG_NOLDS
+                    lds_add_u32((uint32_t)(uintptr_t)&lds.sum[wslot0 + jp], acc0 + acc1);
+#endif
+                    acc0 = acc1 = 0;
                     wp = 0;
                     pmask &= pmask - 1;
                     if (pmask) {
                         jp = (uint32_t)__builtin_ctzll(pmask);
-                        wave_frame(a, lf, jp, false, P);
+                        pframe(a, lf, jp, P);
                     }
                 }
-                issue(buf[d]);
+                issue(b0[d], b1[d]);
             }
         }
     }
 
     // ---- phase C: lane finishes its own frame ----
+    const uint32_t my = wslot0 + (uint32_t)lane;
+    const uint32_t sum_t = lds.sum[my], sum_oob = lds.cnt[kLdsOob + my];
+    lds.sum[my] = 0;
+    lds.cnt[kLdsOob + my] = 0;
     if (stream) {
         if (fi.work & 2) {
-            // udp_csum sums LE words from the UDP start.  sum_t summed the words
+            // tail correction: bytes [keep, 16) of the last checksum chunk lie
+            // past the datagram (the odd-length over-read byte is inside keep)
+            uint32_t corr = 0;
+            if (fi.g.ct >= 0 && fi.g.keep < 16) {
+                const u32x4 t = lds.tail[my];
+                const uint32_t tw4[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const int lo = fi.g.keep - 4 * d;  // bytes of dword d inside the datagram
+                    const uint32_t m = lo <= 0 ? 0xffffffffu : lo >= 4 ? 0u : (0xffffffffu << (8 * lo));
+                    corr = __builtin_amdgcn_udot2(as_u16x2(tw4[d] & m), u16x2{1, 1}, corr, false);
+                }
+            }
+            // udp_csum sums LE words from the UDP start.  tsum summed the words
             // at even addresses: the same words when the UDP header starts at an
             // even address; otherwise every word is byte-swapped, and the one's
             // complement sum of swapped words is the swapped sum (the value
             // mod 0xffff is all udp_csum_ok depends on; + 0xffff keeps the
             // check subtraction from wrapping)
+            const uint32_t tsum = sum_t - fi.head - corr;
             const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
-            uint32_t f = (sum_t & 0xffffu) + (sum_t >> 16);
+            uint32_t f = (tsum & 0xffffu) + (tsum >> 16);
             f = (f & 0xffffu) + (f >> 16);
-            const uint32_t S = even ? sum_t : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
+            const uint32_t S = even ? tsum : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
             if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
                 r.status = DQDK_RX_INVALID_UDP_CSUM;
         }
@@ -553,27 +695,26 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
 
 __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 {
-    __shared__ uint32_t lds_cnt1[kL1Buckets + 1];  // + a dummy slot for masked lanes
+    __shared__ DecodeLds lds;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = rfl((uint32_t)(tid >> 6));
-    if (a.cnt1) {
-        for (int b = tid; b < kL1Buckets + 1; b += kTile)
-            lds_cnt1[b] = 0;
-        __syncthreads();
-    }
+    for (int b = tid; b < kLdsCnt; b += kTile)
+        lds.cnt[b] = 0;
+    lds.sum[tid] = 0;
+    __syncthreads();
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
 
     const uint32_t ntiles = (a.n + 63) / 64;
     for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves)
-        decode_wave_tile(a, t, lane, lds_cnt1);
+        decode_wave_tile(a, t, lane, wave, lds);
 
     if (a.cnt1) {
         __syncthreads();
         for (int b = tid; b < kL1Buckets; b += kTile)
-            if (lds_cnt1[b])
-                atomicAdd(&a.cnt1[b], lds_cnt1[b]);
+            if (lds.cnt[b])
+                atomicAdd(&a.cnt1[b], lds.cnt[b]);
     }
 }
 

@@ -219,6 +219,17 @@ int dqdk_gpu_tristan_summary(const dqdk_gpu_counters_t* const* per_queue, int nq
 int dqdk_gpu_membench_read(const void* d_buf, uint64_t bytes, void* stream, int iters, double* ms_per_pass);
 int dqdk_gpu_membench_atomic(uint32_t* d_table, uint64_t entries, const uint32_t* d_keys, uint64_t nkeys, void* stream,
                              int iters, double* ms_per_pass);
+/* The receive path's memory traffic without its arithmetic: n frames at
+ * `stride` in d_umem, frame_bytes (multiple of 16) read from each and
+ * out_bytes_per_frame written per frame to d_out (16-B aligned; nullable:
+ * read only).  flat = 0: one wave per frame, a frame at a time (the shape
+ * of a per-frame loop); flat = 1: a flat grid-stride walk over all chunks
+ * with four loads in flight per lane and the stores interleaved; flat = 2:
+ * as 0 with 16-B record stores (4 words per lane) instead of 4-B ones;
+ * flat = 3: no frames, n * stride bytes read contiguously and a quarter of
+ * that written (d_out must hold n * stride / 4 bytes). */
+int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame_bytes, uint32_t n, void* d_out,
+                             uint32_t out_bytes_per_frame, int flat, void* stream, int iters, double* ms_per_pass);
 
 /* ---- stage timing (HIP events on the queue stream) ------------------------ */
 /* When enabled, every kernel launch of every batch is bracketed by its own
