@@ -158,6 +158,7 @@ def main():
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
         "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14),
+        "rx_slice_heavy": 0,  # slices redone with u32 bins (none at uniform spectra); bytes counted above
     }
     st = {}
     for name, s in stages.items():
@@ -191,9 +192,14 @@ def main():
     LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, stride, mix_n, d_keys.data_ptr(), 0, 3,
                                                  stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
     pattern["contiguous_mix_4to1"] = round(mix_n * stride * 1.25 / (ms.value * 1e-3) / 1e9, 1)
+    cp_n = min(n, d_keys.numel() * 4 // stride)
+    LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, stride, cp_n, d_keys.data_ptr(), 0, 4,
+                                                 stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
+    pattern["contiguous_copy_1to1"] = round(cp_n * stride * 2 / (ms.value * 1e-3) / 1e9, 1)
     pattern_gbs = pattern["per_frame"]
 
-    hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo") if k in st]
+    hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo",
+                                "rx_slice_heavy") if k in st]
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["avg_ms"] for k in hist_kernels)

@@ -66,7 +66,7 @@ MODES = {"waveform": MODE_WAVEFORM, "listwave": MODE_LISTWAVE, "listmode": MODE_
 F_CSUM, F_BATCH_ABORT, F_PREFILTER, F_NO_HISTO, F_CSUM_WRITEBACK = 1, 2, 4, 8, 16
 F_HISTO_ATOMIC, F_HISTO_PARTITIONED = 32, 64
 KEY_NONE = 0xFFFFFFFF
-TIMING_STAGES = 8
+TIMING_STAGES = 9
 HISTO_CHANNELS, HISTO_HISTS, HISTO_BINS = 1512, 6, 65536
 HISTO_ENTRIES = HISTO_CHANNELS * HISTO_HISTS * HISTO_BINS
 

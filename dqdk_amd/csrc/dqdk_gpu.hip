@@ -46,9 +46,9 @@ int fail_errno(int err, const char* what)
     } while (0)
 
 constexpr int kStages = DQDK_GPU_TIMING_STAGES;
-enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice };
-const char* const kStageNames[kStages] = {"rx_decode", "rx_abort",     "rx_count", "rx_histo_atomic",
-                                          "rx_part1",  "rx_hist_prep", "rx_part2", "rx_slice_histo"};
+enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy };
+const char* const kStageNames[kStages] = {"rx_decode", "rx_abort",     "rx_count", "rx_histo_atomic", "rx_part1",
+                                          "rx_hist_prep", "rx_part2", "rx_slice_histo", "rx_slice_heavy"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
@@ -250,6 +250,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             {
                 StageTimer t(q, kStSlice);
                 hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+            }
+            {
+                StageTimer t(q, kStHeavy);  // usually an empty list: exits at once
+                hipLaunchKernelGGL(rx_slice_heavy_kernel, dim3(q->cu_count), dim3(kSliceThreads), 0, q->stream, ha);
             }
         }
         HIPCHK(hipGetLastError());

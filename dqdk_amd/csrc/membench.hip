@@ -145,6 +145,20 @@ __global__ __launch_bounds__(256) void mix41_kernel(const u32x4_t* __restrict__ 
     }
 }
 
+// Plain 1:1 copy, 16 B per lane, four loads in flight (the guide's float4 copy).
+__global__ __launch_bounds__(256) void copy11_kernel(const u32x4_t* __restrict__ src, uint64_t n16,
+                                                      u32x4_t* __restrict__ dst)
+{
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g + 3 * step < n16; g += 4 * step) {
+        const u32x4_t a = src[g], b = src[g + step], c = src[g + 2 * step], d = src[g + 3 * step];
+        dst[g] = a;
+        dst[g + step] = b;
+        dst[g + 2 * step] = c;
+        dst[g + 3 * step] = d;
+    }
+}
+
 int timed(hipStream_t s, int iters, float* ms, void (*launch)(hipStream_t, const void*), const void* ctx)
 {
     hipEvent_t a, b;
@@ -193,7 +207,10 @@ struct FramesCtx {
 void launch_frames(hipStream_t s, const void* c)
 {
     const FramesCtx* r = (const FramesCtx*)c;
-    if (r->flat == 3)
+    if (r->flat == 4)
+        hipLaunchKernelGGL(copy11_kernel, dim3(r->grid), dim3(256), 0, s, (const u32x4_t*)r->umem,
+                           (uint64_t)r->n * r->stride / 16u, (u32x4_t*)r->out);
+    else if (r->flat == 3)
         hipLaunchKernelGGL(mix41_kernel, dim3(r->grid), dim3(256), 0, s, (const u32x4_t*)r->umem,
                            (uint64_t)r->n * r->stride / 16u, (u32x4_t*)r->out);
     else if (r->flat == 1)
@@ -254,7 +271,7 @@ int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame
         return -EINVAL;
     const uint32_t grid = cu_count() * 8u;
     FramesCtx c{(const uint8_t*)d_umem, stride, frame_bytes, n, (uint32_t*)d_out, out_bytes_per_frame, grid,
-                flat == 3 ? 3 : (flat & 1), flat == 2};
+                flat >= 3 ? flat : (flat & 1), flat == 2};
     float ms = 0.f;
     int rc = timed((hipStream_t)stream, iters, &ms, launch_frames, &c);
     *ms_per_pass = (double)ms / iters;

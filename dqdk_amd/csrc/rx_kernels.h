@@ -18,9 +18,10 @@
  *    - partitioned: rx_part1 (keys -> 284 buckets of 2^21 bins, long runs),
  *      rx_part2 (each 16K-key chunk of a bucket sorted by 16K-bin slice in
  *      LDS, written back as u16 slice-local keys + run offsets),
- *      rx_slice_histo (gathers the slice's runs, LDS histogram, one
- *      coalesced read-modify-write of the slice's 16 KB low-byte plane,
- *      carries of 256 into the u32 base plane).  The table is held as
+ *      rx_slice_histo (gathers the slice's runs, packed-u16 LDS histogram,
+ *      one coalesced read-modify-write of the slice's 16 KB low-byte plane,
+ *      carries of 256 into the u32 base plane; slices with more than 65535
+ *      events are listed and redone with u32 LDS bins by rx_slice_heavy).  The table is held as
  *      value = base[bin] + low[bin] (mod 2^32): the same values as the
  *      reference's u32 table, with a 4x smaller per-batch sweep.
  */
@@ -39,7 +40,7 @@ constexpr int kUnroll = 4;          // 1-KiB windows in flight per wave in phase
 // Partitioned histogram geometry.  Keys < 1512*6*65536 = 594,542,592 < 2^30.
 constexpr int kL1Shift = 21;                                // 2^21 bins (8 MB of table) per bucket
 constexpr int kL1Buckets = 284;                             // ceil(594542592 / 2^21)
-constexpr int kSliceBits = 14;                              // 2^14 bins (64 KB LDS) per slice
+constexpr int kSliceBits = 14;                              // 2^14 bins per slice (32 KB packed-u16 LDS; 64 KB in the u32 form)
 constexpr int kSubs = 1 << (kL1Shift - kSliceBits);         // 128 slices per bucket
 constexpr int kSlices = kL1Buckets * kSubs;                 // 36352 (36288 used)
 constexpr int kPartThreads = 1024;                          // part1/part2 block size
@@ -50,10 +51,12 @@ constexpr int kSliceThreads = 512;
 // u32 scratch words used by the partitioned histogram
 constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket (decode; upper bound)  -- zeroed per batch
 constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket (part1 cursors)   -- zeroed per batch
+constexpr int kOffHeavyN = 574;     // slices listed for the u32 slice form                    -- zeroed per batch
 constexpr int kZeroWords = 576;
 constexpr int kOffOff1 = 576;       // [kL1Buckets + 1] bucket starts in part1/part2 (prep)
 constexpr int kOffIstart = 864;     // [kL1Buckets + 1] first part2 item of each bucket (prep)
-constexpr int kHistScratchWords = 1152;
+constexpr int kOffHeavy = 1152;     // [kSlices] slices with > 65535 events this batch
+constexpr int kHistScratchWords = kOffHeavy + kSlices;
 constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a bucket)
 
 struct RxArgs {
@@ -104,5 +107,6 @@ __global__ void rx_part1_kernel(HistoArgs a);
 __global__ void rx_hist_prep_kernel(HistoArgs a);
 __global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);
+__global__ void rx_slice_heavy_kernel(HistoArgs a);
 
 }  // namespace dqdk

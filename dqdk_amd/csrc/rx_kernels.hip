@@ -1042,24 +1042,34 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 // 16 KB of the table's low-byte plane is loaded up front and read-modify-
 // written once after the LDS histogram is complete, with carries of 256
 // into the u32 base plane (rare: one per 256 increments of a bin).
-__global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
+//
+// Two forms share the code: the common one counts in packed u16 LDS bins
+// (32 KB: four blocks per CU hide the gather latency), valid while the
+// slice receives at most 65535 events in the batch; a slice with more
+// (skewed spectra, hot bins) is appended to a list and redone by the u32
+// form (64 KB LDS) in a second launch over that list.
+struct SliceLds {
+    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads];
+    uint32_t total;
+};
+
+// counters: packed ? u16 pairs (8192 words) : u32 (16384 words)
+template <bool kPacked>
+__device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint32_t* h, SliceLds& sl)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
-    __shared__ uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads];
-    __shared__ uint32_t total;
+    constexpr int kWords = kPacked ? (1 << kSliceBits) / 2 : (1 << kSliceBits);
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     constexpr int kWavesS = kSliceThreads / 64;
-    const uint32_t s = blockIdx.x;
     const uint32_t b = s / kSubs, sub = s % kSubs;
     const uint32_t i0 = a.scratch[kOffIstart + b], i1 = a.scratch[kOffIstart + b + 1];
     if (i0 == i1)
         return;
     const uint32_t bstart = a.scratch[kOffOff1 + b];
     if (tid == 0)
-        total = 0;
+        sl.total = 0;
     u32x4_t* h4 = (u32x4_t*)h;
-    for (int c = tid; c < (1 << kSliceBits) / 4; c += kSliceThreads)
+    for (int c = tid; c < kWords / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
     // events of this slice = sum of its run lengths; the first 512 items' runs stay in LDS
@@ -1068,16 +1078,22 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
         const uint16_t* ro = a.runs + (uint64_t)it * kItemOffs + sub;
         const uint32_t lo = ro[0], hi = ro[1];
         if (it < i0 + kSliceThreads) {
-            s_lo[tid] = lo;
-            s_hi[tid] = hi;
+            sl.s_lo[tid] = lo;
+            sl.s_hi[tid] = hi;
         }
         mine += hi - lo;
     }
     if (mine)
-        atomicAdd(&total, mine);
+        atomicAdd(&sl.total, mine);
     __syncthreads();
+    const uint32_t total = sl.total;
     if (total == 0)
         return;  // no events for this slice: table untouched
+    if (kPacked && total > 0xffffu) {  // a u16 bin could overflow: the u32 form redoes it
+        if (tid == 0)
+            a.scratch[kOffHeavy + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
+        return;
+    }
     const uint64_t sb = (uint64_t)s << kSliceBits;
     u32x4_t* lo4 = (u32x4_t*)(a.lo + sb);
     constexpr int kLoPer = (1 << kSliceBits) / 16 / kSliceThreads;  // 2 x 16 B per thread
@@ -1092,15 +1108,15 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
             __syncthreads();
             if ((uint32_t)tid < nit) {
                 const uint16_t* ro = a.runs + (uint64_t)(ib + tid) * kItemOffs + sub;
-                s_lo[tid] = ro[0];
-                s_hi[tid] = ro[1];
+                sl.s_lo[tid] = ro[0];
+                sl.s_hi[tid] = ro[1];
             }
             __syncthreads();
         }
         for (uint32_t j = (uint32_t)wave; j < nit; j += 2 * kWavesS) {
             const uint32_t j2 = j + kWavesS;
-            const uint32_t alo = s_lo[j], ahi = s_hi[j];
-            const uint32_t blo = j2 < nit ? s_lo[j2] : 0u, bhi = j2 < nit ? s_hi[j2] : 0u;
+            const uint32_t alo = sl.s_lo[j], ahi = sl.s_hi[j];
+            const uint32_t blo = j2 < nit ? sl.s_lo[j2] : 0u, bhi = j2 < nit ? sl.s_hi[j2] : 0u;
             const uint16_t* asrc = a.part2 + bstart + (ib + j - i0) * (uint32_t)kPartChunk;
             const uint16_t* bsrc = a.part2 + bstart + (ib + j2 - i0) * (uint32_t)kPartChunk;
             const uint32_t steps = max(ahi - alo, bhi - blo);
@@ -1114,10 +1130,17 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
                 }
 #pragma unroll
                 for (int g = 0; g < kG; g++) {
-                    if (ka[g] != 0xffffffffu)
-                        atomicAdd(&h[ka[g]], 1u);
-                    if (kb[g] != 0xffffffffu)
-                        atomicAdd(&h[kb[g]], 1u);
+                    if (kPacked) {
+                        if (ka[g] != 0xffffffffu)
+                            atomicAdd(&h[ka[g] >> 1], 1u << ((ka[g] & 1u) << 4));
+                        if (kb[g] != 0xffffffffu)
+                            atomicAdd(&h[kb[g] >> 1], 1u << ((kb[g] & 1u) << 4));
+                    } else {
+                        if (ka[g] != 0xffffffffu)
+                            atomicAdd(&h[ka[g]], 1u);
+                        if (kb[g] != 0xffffffffu)
+                            atomicAdd(&h[kb[g]], 1u);
+                    }
                 }
             }
         }
@@ -1127,16 +1150,34 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
 #pragma unroll
     for (int j = 0; j < kLoPer; j++) {
         const uint32_t b0 = 16u * (uint32_t)(tid + j * kSliceThreads);
-        const u32x4_t* hc = (const u32x4_t*)(h + b0);
+        uint32_t incs[16];
+        if (kPacked) {
+            const u32x4_t* hc = (const u32x4_t*)(h + b0 / 2);
+            const u32x4_t c0 = hc[0], c1 = hc[1];
+            const uint32_t w8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                incs[2 * m] = w8[m] & 0xffffu;
+                incs[2 * m + 1] = w8[m] >> 16;
+            }
+        } else {
+            const u32x4_t* hc = (const u32x4_t*)(h + b0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const u32x4_t c = hc[k];
+                incs[4 * k] = c.x;
+                incs[4 * k + 1] = c.y;
+                incs[4 * k + 2] = c.z;
+                incs[4 * k + 3] = c.w;
+            }
+        }
         uint32_t words[4] = {l[j].x, l[j].y, l[j].z, l[j].w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const u32x4_t inc = hc[k];
-            const uint32_t incs[4] = {inc.x, inc.y, inc.z, inc.w};
             uint32_t nw = 0;
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                const uint32_t nv = ((words[k] >> (8 * m)) & 0xffu) + incs[m];
+                const uint32_t nv = ((words[k] >> (8 * m)) & 0xffu) + incs[4 * k + m];
                 nw |= (nv & 0xffu) << (8 * m);
                 const uint32_t carry = nv & ~0xffu;
                 if (carry)
@@ -1145,6 +1186,25 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs
             words[k] = nw;
         }
         lo4[tid + j * kSliceThreads] = u32x4_t{words[0], words[1], words[2], words[3]};
+    }
+}
+
+__global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t h[(1 << kSliceBits) / 2];
+    __shared__ SliceLds sl;
+    slice_histo<true>(a, blockIdx.x, h, sl);
+}
+
+// Slices with more than 65535 events in the batch (listed by the packed form).
+__global__ void __launch_bounds__(kSliceThreads) rx_slice_heavy_kernel(HistoArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
+    __shared__ SliceLds sl;
+    const uint32_t n = a.scratch[kOffHeavyN];
+    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+        slice_histo<false>(a, a.scratch[kOffHeavy + k], h, sl);
+        __syncthreads();
     }
 }
 

@@ -202,8 +202,8 @@ class RxQueue:
         ms = (C.c_double * ns)()
         cnt = (C.c_uint64 * ns)()
         L.check(L.lib().dqdk_gpu_timing_read(self._h, ms, cnt, ns), "timing_read")
-        return {L.lib().dqdk_gpu_timing_stage_name(k).decode(): {"ms": ms[k], "launches": int(cnt[k])}
-                for k in range(ns)}
+        names = [L.lib().dqdk_gpu_timing_stage_name(k) for k in range(ns)]
+        return {nm.decode(): {"ms": ms[k], "launches": int(cnt[k])} for k, nm in enumerate(names) if nm}
 
 
 def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, directory: str = "") -> str:

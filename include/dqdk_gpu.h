@@ -227,7 +227,8 @@ int dqdk_gpu_membench_atomic(uint32_t* d_table, uint64_t entries, const uint32_t
  * with four loads in flight per lane and the stores interleaved; flat = 2:
  * as 0 with 16-B record stores (4 words per lane) instead of 4-B ones;
  * flat = 3: no frames, n * stride bytes read contiguously and a quarter of
- * that written (d_out must hold n * stride / 4 bytes). */
+ * that written (d_out must hold n * stride / 4 bytes); flat = 4: a plain
+ * 1:1 copy of n * stride bytes into d_out. */
 int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame_bytes, uint32_t n, void* d_out,
                              uint32_t out_bytes_per_frame, int flat, void* stream, int iters, double* ms_per_pass);
 
@@ -236,10 +237,10 @@ int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame
  * pair of hipEvents on the queue stream; stage k is one kernel, named by
  * dqdk_gpu_timing_stage_name(k):
  *   0 rx_decode  1 rx_abort  2 rx_count  3 rx_histo_atomic
- *   4 rx_part1   5 rx_hist_prep  6 rx_part2  7 rx_slice_histo
+ *   4 rx_part1   5 rx_hist_prep  6 rx_part2  7 rx_slice_histo  8 rx_slice_heavy
  * timing_read adds up the completed pairs (after syncing the queue stream),
  * writes stage_ms[k] / counts[k] (launches) for k < nstages and clears them. */
-#define DQDK_GPU_TIMING_STAGES 8
+#define DQDK_GPU_TIMING_STAGES 9
 int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on);
 int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages);
 const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */

@@ -213,6 +213,9 @@ def test_skewed_histogram(hpath):
         ev[..., 6][m] = e6
         ev[..., 8][m] = hc
     cfg = D.RxConfig(payloadsz=1458, flags=hpath)  # no checksum: payload edited
+    _, _, okeys = O.rx_batch(umem.copy(), desc, 1458)
+    per_slice = np.bincount((okeys[okeys != D.KEY_NONE] >> 14).astype(np.int64))
+    assert per_slice.max() > 0xFFFF  # the partitioned path must take its u32 (rx_slice_heavy) form
     compare(umem, desc, cfg, check_hist=True)
 
 
@@ -302,7 +305,7 @@ def test_full_size_properties(L, stride, payloadsz):
 @pytest.mark.parametrize("hpath,kernels", [
     (D.F_HISTO_ATOMIC, {"rx_decode", "rx_abort", "rx_count", "rx_histo_atomic"}),
     (D.F_HISTO_PARTITIONED, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_hist_prep", "rx_part2",
-                             "rx_slice_histo"})], ids=["atomic", "partitioned"])
+                             "rx_slice_histo", "rx_slice_heavy"})], ids=["atomic", "partitioned"])
 def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels):
     _need_gpu()
     umem, desc = D.synth_umem(1024, 1500, 4096)
