@@ -233,11 +233,12 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         } else {
             const uint64_t nkeys = (uint64_t)n * q->E;
             const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
-            const uint32_t grid_p = std::min<uint32_t>(chunks, (uint32_t)q->cu_count * 2u);
+            const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
+                                                       (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
             const uint32_t grid_l2 = std::min<uint32_t>(chunks + kL1Buckets, (uint32_t)q->cu_count * 2u);
             {
                 StageTimer t(q, kStPart1);
-                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kPartThreads), 0, q->stream, ha);
+                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ha);
             }
             {
                 StageTimer t(q, kStPrep);
@@ -449,8 +450,9 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
             const size_t items = nk / kPartChunk + kL1Buckets + 1;
-            if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess || (e = hipMalloc(&q->d_part1, nk * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part2, nk * 2)) != hipSuccess ||
+            if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part1, (nk + kStagePad) * 4)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part2, (nk + kStagePad) * 2)) != hipSuccess ||
                 (e = hipMalloc(&q->d_runs, items * kItemOffs * sizeof(uint16_t))) != hipSuccess ||
                 (e = hipMalloc(&q->d_hscratch, kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));

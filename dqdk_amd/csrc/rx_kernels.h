@@ -47,6 +47,16 @@ constexpr int kPartThreads = 1024;                          // part1/part2 block
 constexpr int kPartKeysPerThread = 16;
 constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 16384 keys staged in LDS
 constexpr int kSliceThreads = 512;
+#ifndef DQDK_P1_KEYS
+#define DQDK_P1_KEYS 32
+#endif
+constexpr int kP1Threads = 1024;                            // part1 block size
+constexpr int kP1Keys = DQDK_P1_KEYS;                       // keys per thread
+constexpr int kP1Chunk = kP1Threads * kP1Keys;              // keys staged in LDS per block
+constexpr int kP1MinWaves = kP1Keys > 16 ? 4 : 8;           // waves per SIMD: 1 or 2 blocks per CU
+constexpr int kP1BlocksPerCu = kP1MinWaves / 4;
+constexpr uint32_t kBucketAlign = 8;  // bucket starts in part1/part2 rounded to 8 keys (16-B part2 stores)
+constexpr uint32_t kStagePad = kL1Buckets * kBucketAlign;  // extra part1/part2 entries for that padding
 
 // u32 scratch words used by the partitioned histogram
 constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket (decode; upper bound)  -- zeroed per batch

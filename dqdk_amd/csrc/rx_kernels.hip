@@ -842,7 +842,8 @@ __global__ void __launch_bounds__(256) rx_histo_atomic_kernel(HistoArgs a)
 
 // Exclusive scan of src[0..n) (n <= 320) into dst[0..n], dst[n] = total, by
 // wave 0 of the block (5 entries per lane).  Caller syncs afterwards.
-__device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* dst, int n, bool src_global)
+__device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* dst, int n, bool src_global,
+                                                uint32_t align = 1)
 {
     if (threadIdx.x >= 64)
         return;
@@ -852,6 +853,7 @@ __device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* d
     for (int j = 0; j < 5; j++) {
         const int i = lane * 5 + j;
         v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) : 0u;
+        v[j] = (v[j] + align - 1) & ~(align - 1);
         sum += v[j];
     }
     uint32_t incl = sum;
@@ -888,68 +890,73 @@ __device__ __forceinline__ int find_run(const uint32_t* off, int nb, uint32_t p)
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 // Level 1: keys (frame order) -> part1, grouped by bucket = key >> 21.
-// A block stages 16K keys in LDS sorted by bucket, reserves each bucket's
-// run with one global atomic, and writes the runs out contiguously.
-__global__ void __launch_bounds__(kPartThreads, 8) rx_part1_kernel(HistoArgs a)  // 2 blocks/CU
+// A block stages kP1Chunk keys in LDS sorted by bucket, reserves each
+// bucket's run with one global atomic, and writes the runs out
+// contiguously.  The keys of a thread are dword buffer loads issued back to
+// back (lane-contiguous, out-of-range lanes read 0 and are dropped by
+// index); the counting atomic returns each key's rank inside its bucket, so
+// the scatter is a plain LDS store; the run reservations (284 returning
+// atomics on 284 shared cursors, the contended step) are waited for only
+// after the scatter.  One 32K-key chunk per block (128 KB of LDS, one block
+// per CU) halves the reservations per key of a 16K chunk and doubles the
+// average run written per bucket.
+__global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(HistoArgs a)
 {
-    __shared__ uint32_t stage[kPartChunk];
+    __shared__ uint32_t stage[kP1Chunk];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t lcnt[kL1Buckets];
     __shared__ uint32_t loff[kL1Buckets + 1];
-    __shared__ uint32_t gpos[kL1Buckets];
+    __shared__ uint32_t gdel[kL1Buckets];  // global position - LDS position of each bucket's run
     const int tid = threadIdx.x;
     const uint32_t limit = frames_limit(a);
     const uint32_t total = limit * a.E;
+    const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
-    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true);
-    for (uint32_t base = blockIdx.x * (uint32_t)kPartChunk; base < total; base += gridDim.x * (uint32_t)kPartChunk) {
-        for (int b = tid; b < kL1Buckets; b += kPartThreads)
+    constexpr int kOwn = (kL1Buckets + kP1Threads - 1) / kP1Threads;  // buckets reserved per thread (1)
+    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
+    for (uint32_t base = blockIdx.x * (uint32_t)kP1Chunk; base < total; base += step) {
+        const uint32_t nk = min(total - base, (uint32_t)kP1Chunk);
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + base, (uint64_t)nk * 4u);
+        uint32_t key[kP1Keys];
+#pragma unroll
+        for (int j = 0; j < kP1Keys; j++)
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kP1Threads * 4, 0);
+        for (int b = tid; b < kL1Buckets; b += kP1Threads)
             lcnt[b] = 0;
         __syncthreads();
-        uint32_t key[kPartKeysPerThread];
+        uint32_t rank[kP1Keys / 2];  // two u16 ranks per word (rank < kP1Chunk <= 65536)
 #pragma unroll
-        for (int j = 0; j < kPartKeysPerThread / 4; j++) {
-            const uint32_t p0 = base + (uint32_t)(j * kPartThreads + tid) * 4;
-            u32x4_t v = {DQDK_KEY_NONE, DQDK_KEY_NONE, DQDK_KEY_NONE, DQDK_KEY_NONE};
-            if (p0 + 3 < total) {
-                v = *(const u32x4_t*)(a.keys + p0);
-            } else {
-                if (p0 + 0 < total) v.x = a.keys[p0 + 0];
-                if (p0 + 1 < total) v.y = a.keys[p0 + 1];
-                if (p0 + 2 < total) v.z = a.keys[p0 + 2];
-            }
-            key[4 * j + 0] = v.x;
-            key[4 * j + 1] = v.y;
-            key[4 * j + 2] = v.z;
-            key[4 * j + 3] = v.w;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                uint32_t& k = key[4 * j + c];
-                if (!(p0 + c < total))
-                    k = DQDK_KEY_NONE;  // non-OK frames already hold KEY_NONE
-                if (k != DQDK_KEY_NONE)
-                    atomicAdd(&lcnt[k >> kL1Shift], 1u);
-            }
+        for (int j = 0; j < kP1Keys; j++) {
+            // non-OK frames already hold KEY_NONE; lanes past the chunk are dropped
+            if (!((uint32_t)(j * kP1Threads + tid) < nk))
+                key[j] = DQDK_KEY_NONE;
+            const uint32_t r = key[j] != DQDK_KEY_NONE ? atomicAdd(&lcnt[key[j] >> kL1Shift], 1u) : 0u;
+            rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kL1Buckets, false);
         __syncthreads();
-        for (int b = tid; b < kL1Buckets; b += kPartThreads) {
-            if (lcnt[b])
-                gpos[b] = off1[b] + atomicAdd(&cur1[b], lcnt[b]);
-            lcnt[b] = loff[b];  // reused as the LDS stage cursor of each bucket
+        uint32_t g[kOwn];
+#pragma unroll
+        for (int o = 0; o < kOwn; o++) {
+            const int b = tid + o * kP1Threads;
+            g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], lcnt[b]) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kP1Keys; j++)
+            if (key[j] != DQDK_KEY_NONE)
+                stage[loff[key[j] >> kL1Shift] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] = key[j];
+#pragma unroll
+        for (int o = 0; o < kOwn; o++) {
+            const int b = tid + o * kP1Threads;
+            if (b < kL1Buckets)
+                gdel[b] = off1[b] + g[o] - loff[b];
         }
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)
-            if (key[j] != DQDK_KEY_NONE)
-                stage[atomicAdd(&lcnt[key[j] >> kL1Shift], 1u)] = key[j];
-        __syncthreads();
         const uint32_t nkeys = loff[kL1Buckets];
-        for (uint32_t p = tid; p < nkeys; p += kPartThreads) {
+        for (uint32_t p = tid; p < nkeys; p += kP1Threads) {
             const uint32_t k = stage[p];
-            const uint32_t b = k >> kL1Shift;
-            a.part1[gpos[b] + (p - loff[b])] = k;
+            a.part1[p + gdel[k >> kL1Shift]] = k;
         }
         __syncthreads();
     }
@@ -959,7 +966,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part1_kernel(HistoArgs a) 
 // (scan of ceil(bucket length / chunk)), once per batch.
 __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 {
-    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true);
+    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign);
     const int lane = threadIdx.x;
     uint32_t v[5], sum = 0;
 #pragma unroll
@@ -990,7 +997,7 @@ __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 // slice-local keys, with the run starts of its 128 slices.
 __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 2 blocks/CU
 {
-    __shared__ uint16_t stage[kPartChunk];
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
     __shared__ uint32_t istart[kL1Buckets + 1];
     __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1];
     const int tid = threadIdx.x;
@@ -1011,7 +1018,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         uint32_t key[kPartKeysPerThread];
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)  // out-of-range lanes read 0 (dropped below)
-            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)(j * kPartThreads + tid) * 4u, 0, 0);
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
             if ((uint32_t)(j * kPartThreads + tid) < nk)
@@ -1030,8 +1037,12 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 stage[atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         __syncthreads();
-        for (uint32_t p = tid; p < nk; p += kPartThreads)
-            a.part2[base + p] = stage[p];
+        // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
+        // stale LDS past nk lands in the bucket's padding (never read)
+        const u32x4_t* st4 = (const u32x4_t*)stage;
+        u32x4_t* dst4 = (u32x4_t*)(a.part2 + base);
+        for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
+            dst4[p] = st4[p];
         __syncthreads();
     }
 }
