@@ -152,8 +152,9 @@ def main():
         "rx_abort": 8 * n,
         "rx_count": 8 * n,
         "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
-        "rx_part1": 8 * n + 8 * K,
-        "rx_hist_prep": 0,
+        "rx_part1": 8 * K,  # keys read + bucket runs written (+ two 1.1 KB count rows per unit)
+        # count scan: the decode's per-tile bucket-count rows prefixed in place, group rows summed twice
+        "rx_hist_prep": 8 * 288 * (-(-n // 64)) + 12 * 288 * (-(-n // 4096)),
         "rx_part2": 6 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
@@ -174,6 +175,15 @@ def main():
 
     from dqdk_amd import _lib as LIB
     ms = C.c_double()
+    # random-atomic bound of the histogram, on this batch's records (before the
+    # pattern benchmarks below reuse the records buffer as their sink)
+    atomic_gupd = None
+    if histo and E:
+        scratch = torch.zeros(D.HISTO_ENTRIES, dtype=torch.int32, device=dev)
+        LIB.check(LIB.lib().dqdk_gpu_membench_atomic(scratch.data_ptr(), D.HISTO_ENTRIES, d_keys.data_ptr(), K,
+                                                     stream.cuda_stream, 3, C.byref(ms)), "membench_atomic")
+        del scratch
+        atomic_gupd = K / (ms.value * 1e-3) / 1e9
     LIB.check(LIB.lib().dqdk_gpu_membench_read(d_umem.data_ptr(), umem_bytes // 16 * 16, stream.cuda_stream, 5,
                                                C.byref(ms)), "membench_read")
     stream_gbs = umem_bytes // 16 * 16 / (ms.value * 1e-3) / 1e9
@@ -203,11 +213,6 @@ def main():
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["avg_ms"] for k in hist_kernels)
-        scratch = torch.zeros(D.HISTO_ENTRIES, dtype=torch.int32, device=dev)
-        LIB.check(LIB.lib().dqdk_gpu_membench_atomic(scratch.data_ptr(), D.HISTO_ENTRIES, d_keys.data_ptr(), K,
-                                                     stream.cuda_stream, 3, C.byref(ms)), "membench_atomic")
-        del scratch
-        atomic_gupd = K / (ms.value * 1e-3) / 1e9
         gupd = K / (h_ms * 1e-3) / 1e9
         histogram = {"kernels": hist_kernels, "updates_per_batch": K, "touched_slices": touched,
                      "ms": round(h_ms, 4), "Gupd_s": round(gupd, 2),

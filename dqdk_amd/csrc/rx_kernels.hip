@@ -843,7 +843,7 @@ __global__ void __launch_bounds__(256) rx_histo_atomic_kernel(HistoArgs a)
 // Exclusive scan of src[0..n) (n <= 320) into dst[0..n], dst[n] = total, by
 // wave 0 of the block (5 entries per lane).  Caller syncs afterwards.
 __device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* dst, int n, bool src_global,
-                                                uint32_t align = 1)
+                                                uint32_t align = 1, uint32_t slack = 0)
 {
     if (threadIdx.x >= 64)
         return;
@@ -852,7 +852,7 @@ __device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* d
 #pragma unroll
     for (int j = 0; j < 5; j++) {
         const int i = lane * 5 + j;
-        v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) : 0u;
+        v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) + slack : 0u;
         v[j] = (v[j] + align - 1) & ~(align - 1);
         sum += v[j];
     }
@@ -913,7 +913,9 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
     constexpr int kOwn = (kL1Buckets + kP1Threads - 1) / kP1Threads;  // buckets reserved per thread (1)
-    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
+    // room for every chunk's KEY_NONE padding of every run
+    const uint32_t slack = (kRunAlign - 1) * ((total + kP1Chunk - 1) / kP1Chunk);
+    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign, slack);
     for (uint32_t base = blockIdx.x * (uint32_t)kP1Chunk; base < total; base += step) {
         const uint32_t nk = min(total - base, (uint32_t)kP1Chunk);
         const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + base, (uint64_t)nk * 4u);
@@ -940,7 +942,8 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
 #pragma unroll
         for (int o = 0; o < kOwn; o++) {
             const int b = tid + o * kP1Threads;
-            g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], lcnt[b]) : 0u;
+            g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], (lcnt[b] + kRunAlign - 1) / kRunAlign * kRunAlign)
+                                             : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kP1Keys; j++)
@@ -958,6 +961,15 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
             const uint32_t k = stage[p];
             a.part1[p + gdel[k >> kL1Shift]] = k;
         }
+        if (kRunAlign > 1) {  // runs end on a kRunAlign boundary: no line is shared by two blocks' runs
+#pragma unroll
+            for (int o = 0; o < kOwn; o++) {
+                const int b = tid + o * kP1Threads;
+                if (b < kL1Buckets && lcnt[b])
+                    for (uint32_t p = off1[b] + g[o] + lcnt[b]; p % kRunAlign; p++)
+                        a.part1[p] = DQDK_KEY_NONE;
+            }
+        }
         __syncthreads();
     }
 }
@@ -966,7 +978,8 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
 // (scan of ceil(bucket length / chunk)), once per batch.
 __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 {
-    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign);
+    const uint32_t slack = (kRunAlign - 1) * ((frames_limit(a) * a.E + kP1Chunk - 1) / kP1Chunk);  // as part1
+    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign, slack);
     const int lane = threadIdx.x;
     uint32_t v[5], sum = 0;
 #pragma unroll
@@ -1020,9 +1033,13 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         for (int j = 0; j < kPartKeysPerThread; j++)  // out-of-range lanes read 0 (dropped below)
             key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
 #pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)
-            if ((uint32_t)(j * kPartThreads + tid) < nk)
+        for (int j = 0; j < kPartKeysPerThread; j++) {
+            // lanes past the chunk (and part1's KEY_NONE padding, kRunAlign > 1) are dropped
+            if (!((uint32_t)(j * kPartThreads + tid) < nk))
+                key[j] = DQDK_KEY_NONE;
+            if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
                 atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u);
+        }
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kSubs, false);
         __syncthreads();
@@ -1033,7 +1050,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
-            if ((uint32_t)(j * kPartThreads + tid) < nk)
+            if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
                 stage[atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         __syncthreads();
@@ -1049,7 +1066,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 
 // Level 3: one block per 16K-bin slice.  The run offsets of the bucket's
 // items (<= 512 at a time) are staged in LDS first, so gathering a run is
-// one dependent load, and each wave gathers two items at once; the slice's
+// one dependent load, and each wave gathers four items at once; the slice's
 // 16 KB of the table's low-byte plane is loaded up front and read-modify-
 // written once after the LDS histogram is complete, with carries of 256
 // into the u32 base plane (rare: one per 256 increments of a bin).
@@ -1063,6 +1080,15 @@ struct SliceLds {
     uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads];
     uint32_t total;
 };
+
+template <bool kPacked>
+__device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
+{
+    if (kPacked)
+        atomicAdd(&h[k >> 1], 1u << ((k & 1u) << 4));
+    else
+        atomicAdd(&h[k], 1u);
+}
 
 // counters: packed ? u16 pairs (8192 words) : u32 (16384 words)
 template <bool kPacked>
@@ -1112,7 +1138,18 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
 #pragma unroll
     for (int j = 0; j < kLoPer; j++)
         l[j] = lo4[tid + j * kSliceThreads];
-    constexpr int kG = 4;  // loads in flight per lane per item
+    // each wave gathers kNI items at once, kKG dwords (two keys) per lane per
+    // item per pass (256 keys: a whole typical run), so a block takes its
+    // items in rounds of kNI * kWavesS; runs start at any key: dword loads
+    // from the run's first even key, halves outside the run are dropped
+#ifndef DQDK_SLICE_NI
+#define DQDK_SLICE_NI 4
+#endif
+#ifndef DQDK_SLICE_KG
+#define DQDK_SLICE_KG 2
+#endif
+    constexpr int kNI = DQDK_SLICE_NI;
+    constexpr int kKG = DQDK_SLICE_KG;
     for (uint32_t ib = i0; ib < i1; ib += kSliceThreads) {
         const uint32_t nit = min(i1 - ib, (uint32_t)kSliceThreads);
         if (ib != i0) {  // buckets with more than 512 items (skewed data)
@@ -1124,35 +1161,40 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             }
             __syncthreads();
         }
-        for (uint32_t j = (uint32_t)wave; j < nit; j += 2 * kWavesS) {
-            const uint32_t j2 = j + kWavesS;
-            const uint32_t alo = sl.s_lo[j], ahi = sl.s_hi[j];
-            const uint32_t blo = j2 < nit ? sl.s_lo[j2] : 0u, bhi = j2 < nit ? sl.s_hi[j2] : 0u;
-            const uint16_t* asrc = a.part2 + bstart + (ib + j - i0) * (uint32_t)kPartChunk;
-            const uint16_t* bsrc = a.part2 + bstart + (ib + j2 - i0) * (uint32_t)kPartChunk;
-            const uint32_t steps = max(ahi - alo, bhi - blo);
-            for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kG) {
-                uint32_t ka[kG], kb[kG];
+        for (uint32_t j = (uint32_t)wave; j < nit; j += kNI * kWavesS) {
+            uint32_t klo[kNI], khi[kNI], dlo[kNI], dhi[kNI];
+            const uint32_t* src[kNI];
+            uint32_t steps = 0;
 #pragma unroll
-                for (int g = 0; g < kG; g++) {
-                    const uint32_t pa = alo + p0 + 64 * g + lane, pb = blo + p0 + 64 * g + lane;
-                    ka[g] = pa < ahi ? (uint32_t)asrc[pa] : 0xffffffffu;
-                    kb[g] = pb < bhi ? (uint32_t)bsrc[pb] : 0xffffffffu;
-                }
+            for (int q = 0; q < kNI; q++) {
+                const uint32_t jj = j + q * kWavesS;
+                klo[q] = jj < nit ? sl.s_lo[jj] : 0u;
+                khi[q] = jj < nit ? sl.s_hi[jj] : 0u;
+                dlo[q] = klo[q] >> 1;
+                dhi[q] = (khi[q] + 1) >> 1;
+                // item chunks start at multiples of kBucketAlign keys: dword-aligned
+                src[q] = (const uint32_t*)(a.part2 + bstart + (ib + jj - i0) * (uint32_t)kPartChunk);
+                steps = max(steps, dhi[q] - dlo[q]);
+            }
+            for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
+                uint32_t w[kNI][kKG];
 #pragma unroll
-                for (int g = 0; g < kG; g++) {
-                    if (kPacked) {
-                        if (ka[g] != 0xffffffffu)
-                            atomicAdd(&h[ka[g] >> 1], 1u << ((ka[g] & 1u) << 4));
-                        if (kb[g] != 0xffffffffu)
-                            atomicAdd(&h[kb[g] >> 1], 1u << ((kb[g] & 1u) << 4));
-                    } else {
-                        if (ka[g] != 0xffffffffu)
-                            atomicAdd(&h[ka[g]], 1u);
-                        if (kb[g] != 0xffffffffu)
-                            atomicAdd(&h[kb[g]], 1u);
+                for (int q = 0; q < kNI; q++)
+#pragma unroll
+                    for (int g = 0; g < kKG; g++) {
+                        const uint32_t d = dlo[q] + p0 + 64 * g + lane;
+                        w[q][g] = d < dhi[q] ? src[q][d] : 0u;
                     }
-                }
+#pragma unroll
+                for (int q = 0; q < kNI; q++)
+#pragma unroll
+                    for (int g = 0; g < kKG; g++) {
+                        const uint32_t k0 = 2 * (dlo[q] + p0 + 64 * g + lane);  // key index of the low half
+                        if (k0 >= klo[q] && k0 < khi[q])
+                            slice_count<kPacked>(h, w[q][g] & 0xffffu);
+                        if (k0 + 1 >= klo[q] && k0 + 1 < khi[q])
+                            slice_count<kPacked>(h, w[q][g] >> 16);
+                    }
             }
         }
     }

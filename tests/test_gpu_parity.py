@@ -113,6 +113,7 @@ CASES = [
     (1500, 4096, True, 1458, D.MODE_WAVEFORM, 0),               # no histogram
     (1500, 4096, True, 1458, D.MODE_ENERGYHISTO, D.F_NO_HISTO | D.F_CSUM),
     (1500, 4096, True, 8, D.MODE_ENERGYHISTO, D.F_CSUM),        # E = 0
+    (9000, 9216, True, 12000, D.MODE_ENERGYHISTO, D.F_CSUM),    # E = 750: part1 stages a tile in two chunks
 ]
 
 
