@@ -889,6 +889,15 @@ __device__ __forceinline__ int find_run(const uint32_t* off, int nb, uint32_t p)
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef DQDK_P1_PIPE
+#define DQDK_P1_PIPE 1
+#endif
+constexpr bool kP1Pipe = DQDK_P1_PIPE;  // part1 loads chunk c+1 while chunk c is written out
+#ifndef DQDK_P2_PIPE
+#define DQDK_P2_PIPE 1
+#endif
+constexpr bool kP2Pipe = DQDK_P2_PIPE;  // part2 loads item i+1 while item i is written out
+
 // Level 1: keys (frame order) -> part1, grouped by bucket = key >> 21.
 // A block stages kP1Chunk keys in LDS sorted by bucket, reserves each
 // bucket's run with one global atomic, and writes the runs out
@@ -916,13 +925,20 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     // room for every chunk's KEY_NONE padding of every run
     const uint32_t slack = (kRunAlign - 1) * ((total + kP1Chunk - 1) / kP1Chunk);
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign, slack);
-    for (uint32_t base = blockIdx.x * (uint32_t)kP1Chunk; base < total; base += step) {
-        const uint32_t nk = min(total - base, (uint32_t)kP1Chunk);
-        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + base, (uint64_t)nk * 4u);
-        uint32_t key[kP1Keys];
+    uint32_t key[kP1Keys];
+    auto load = [&](uint32_t b0) {
+        const uint32_t n0 = min(total - b0, (uint32_t)kP1Chunk);
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + b0, (uint64_t)n0 * 4u);
 #pragma unroll
         for (int j = 0; j < kP1Keys; j++)
             key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kP1Threads * 4, 0);
+    };
+    if (kP1Pipe && blockIdx.x * (uint32_t)kP1Chunk < total)
+        load(blockIdx.x * (uint32_t)kP1Chunk);
+    for (uint32_t base = blockIdx.x * (uint32_t)kP1Chunk; base < total; base += step) {
+        const uint32_t nk = min(total - base, (uint32_t)kP1Chunk);
+        if (!kP1Pipe)
+            load(base);
         for (int b = tid; b < kL1Buckets; b += kP1Threads)
             lcnt[b] = 0;
         __syncthreads();
@@ -955,6 +971,10 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
             if (b < kL1Buckets)
                 gdel[b] = off1[b] + g[o] - loff[b];
         }
+        // the next chunk's keys load while this one is written out (key[] is
+        // free once scattered)
+        if (kP1Pipe && base + step < total)
+            load(base + step);
         __syncthreads();
         const uint32_t nkeys = loff[kL1Buckets];
         for (uint32_t p = tid; p < nkeys; p += kP1Threads) {
@@ -1008,7 +1028,7 @@ __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 // Level 2: each item = one 16K-key chunk of one bucket's part1 run, sorted
 // by slice ((key >> 14) & 127) in LDS and written back in place as u16
 // slice-local keys, with the run starts of its 128 slices.
-__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 2 blocks/CU
+__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
     __shared__ uint32_t istart[kL1Buckets + 1];
@@ -1018,20 +1038,35 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         istart[b] = a.scratch[kOffIstart + b];
     __syncthreads();
     const uint32_t nitems = istart[kL1Buckets];
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    uint32_t key[kPartKeysPerThread];
+    // item -> its keys [base, base + nk) in part1/part2; loads them into key[]
+    // (out-of-range lanes read 0 and are dropped below)
+    auto geo = [&](uint32_t item, uint32_t& nk, uint32_t& base) {
         const int b = find_run(istart, kL1Buckets, item);
         const uint32_t c0 = (item - istart[b]) * (uint32_t)kPartChunk;
-        const uint32_t len = a.scratch[kOffCur1 + b];
-        const uint32_t nk = min(len - c0, (uint32_t)kPartChunk);
-        const uint32_t base = a.scratch[kOffOff1 + b] + c0;
+        nk = min(a.scratch[kOffCur1 + b] - c0, (uint32_t)kPartChunk);
+        base = a.scratch[kOffOff1 + b] + c0;
+    };
+    auto load = [&](uint32_t base, uint32_t nk) {
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+    };
+    uint32_t nk_next = 0, base_next = 0;
+    if (kP2Pipe && blockIdx.x < nitems) {
+        geo(blockIdx.x, nk_next, base_next);
+        load(base_next, nk_next);
+    }
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        uint32_t nk = nk_next, base = base_next;
+        if (!kP2Pipe)
+            geo(item, nk, base);
         if (tid < kSubs)
             lcnt[tid] = 0;
         __syncthreads();
-        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
-        uint32_t key[kPartKeysPerThread];
-#pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)  // out-of-range lanes read 0 (dropped below)
-            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+        if (!kP2Pipe)
+            load(base, nk);
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
             // lanes past the chunk (and part1's KEY_NONE padding, kRunAlign > 1) are dropped
@@ -1053,6 +1088,11 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
                 stage[atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
+        // the next item's keys load while this one is written out
+        if (kP2Pipe && item + gridDim.x < nitems) {
+            geo(item + gridDim.x, nk_next, base_next);
+            load(base_next, nk_next);
+        }
         __syncthreads();
         // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
         // stale LDS past nk lands in the bucket's padding (never read)
