@@ -346,6 +346,9 @@ constexpr int kRingW = DQDK_RINGW;
 #ifndef DQDK_ST_AUX
 #define DQDK_ST_AUX 0
 #endif
+#ifndef DQDK_DEC_SINK
+#define DQDK_DEC_SINK 0
+#endif
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -439,7 +442,7 @@ __device__ __forceinline__ void lds_add_u32(uint32_t lds_addr, uint32_t v)
 
 // One event per 16-B chunk v (event byte 2 at byte r of v.x): key record
 // store, then one LDS count: the key's L1 bucket, the frame's OOB slot for
-// an out-of-bounds event, the sink for a lane without an event.
+// an out-of-bounds event (lanes without an event do no LDS count).
 __device__ __forceinline__ void decode_chunk(const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef, uint32_t kbase,
                                              uint32_t oob_slot, __amdgpu_buffer_rsrc_t keys_rsrc, uint32_t* cnt)
 {
@@ -454,9 +457,14 @@ __device__ __forceinline__ void decode_chunk(const u32x4& v, uint32_t r, uint32_
     const bool has = e < Ef;
     __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has ? kbase + 4u * e : kOOB, 0, DQDK_ST_AUX);
     // KEY_NONE >> kL1Shift = 2047 > oob_slot > every bucket
+#if DQDK_DEC_SINK  // A/B only: lanes without an event count into one sink word
     const uint32_t idx = has ? min(key >> kL1Shift, oob_slot) : (uint32_t)kLdsSink;
-#ifndef DQDK_DIAG_NOLDS  // timing diagnostic only
     atomicAdd(&cnt[idx], 1u);
+#else
+    // lanes without an event stay out of the LDS: at 1500 B 37 of a window's
+    // 128 chunk slots carry none, and one shared sink word serialised them
+    if (has)
+        atomicAdd(&cnt[min(key >> kL1Shift, oob_slot)], 1u);
 #endif
 }
 
