@@ -105,6 +105,7 @@ struct dqdk_gpu_queue {
     std::vector<Reg> regs;
     // stage timing
     int timing = 0;
+    uint32_t stage_mask = ~0u;  // stages bracketed while timing is on
     std::vector<hipEvent_t> ev_free;
     struct Pending {
         int stage;
@@ -134,7 +135,7 @@ struct StageTimer {
     hipEvent_t a = nullptr, b = nullptr;
     StageTimer(dqdk_gpu_queue* q_, int s) : q(q_), stage(s)
     {
-        if (q->timing && ev_get(q, &a) == 0 && ev_get(q, &b) == 0)
+        if (q->timing && ((q->stage_mask >> stage) & 1u) && ev_get(q, &a) == 0 && ev_get(q, &b) == 0)
             (void)hipEventRecord(a, q->stream);
     }
     ~StageTimer()
@@ -690,6 +691,14 @@ int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on)
     if (!q)
         return -EINVAL;
     q->timing = on ? 1 : 0;
+    return 0;
+}
+
+int dqdk_gpu_timing_stages(dqdk_gpu_queue_t* q, uint32_t stage_mask)
+{
+    if (!q)
+        return -EINVAL;
+    q->stage_mask = stage_mask;
     return 0;
 }
 

@@ -196,6 +196,14 @@ class RxQueue:
     def enable_timing(self, on: bool = True) -> None:
         L.check(L.lib().dqdk_gpu_timing_enable(self._h, int(on)), "timing_enable")
 
+    def timing_stages(self, names=None) -> None:
+        """Time only the named stages (None: all)."""
+        mask = 0xFFFFFFFF
+        if names is not None:
+            all_names = [L.lib().dqdk_gpu_timing_stage_name(k).decode() for k in range(L.TIMING_STAGES)]
+            mask = sum(1 << all_names.index(n) for n in names)
+        L.check(L.lib().dqdk_gpu_timing_stages(self._h, mask), "timing_stages")
+
     def read_timing(self) -> dict:
         """Per-kernel HIP-event totals since the last read: {kernel: {ms, launches}}."""
         ns = L.TIMING_STAGES

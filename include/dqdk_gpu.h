@@ -242,6 +242,9 @@ int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame
  * writes stage_ms[k] / counts[k] (launches) for k < nstages and clears them. */
 #define DQDK_GPU_TIMING_STAGES 9
 int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on);
+/* Restrict the bracketing to the stages whose bit is set in stage_mask
+ * (default: all); the others launch without events in between. */
+int dqdk_gpu_timing_stages(dqdk_gpu_queue_t* q, uint32_t stage_mask);
 int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages);
 const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
 
