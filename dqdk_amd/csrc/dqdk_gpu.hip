@@ -13,6 +13,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -209,7 +210,8 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     {
         StageTimer t(q, kStCount);
-        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
+        const uint32_t grid_c = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count);
+        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_c), dim3(256), 0, q->stream, ca);
     }
     HIPCHK(hipGetLastError());
 

@@ -764,16 +764,15 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
 #pragma unroll
     for (int k = 0; k < C_N; k++)
         c[k] = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
-        const dqdk_gpu_rx_result_t r = a.res[i];
+    auto count = [&](uint32_t i, const dqdk_gpu_rx_result_t& r) {
         const uint32_t st = r.status;
         if (!in_batch(st)) {
             c[C_FILT]++;
-            continue;
+            return;
         }
         c[C_FRAMES]++;
         if (i >= limit)
-            continue;
+            return;
         c[C_PKTS]++;
         c[C_IP] += (st == DQDK_RX_INVALID_IP || st == DQDK_RX_INVALID_IP_CSUM);
         c[C_UDP] += (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM);
@@ -784,6 +783,20 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
             c[C_EVENTS] += a.E;
             c[C_OOB] += a.histo ? r.oob_events : 0u;
         }
+    };
+    // one block per CU (few blocks: every block ends in 20 device atomics on
+    // the same 20 words), four result loads in flight per thread
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < a.n; i0 += 4 * stride) {
+        dqdk_gpu_rx_result_t r[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i0 + u * stride < a.n)
+                r[u] = a.res[i0 + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i0 + u * stride < a.n)
+                count(i0 + u * stride, r[u]);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -1075,26 +1088,27 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         __syncthreads();
         if (!kP2Pipe)
             load(base, nk);
+        // the counting atomic returns each key's rank inside its slice, so the
+        // scatter after the scan is a plain LDS store
+        uint32_t rank[kPartKeysPerThread / 2];  // two u16 ranks per word (rank < kPartChunk)
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
             // lanes past the chunk (and part1's KEY_NONE padding, kRunAlign > 1) are dropped
             if (!((uint32_t)(j * kPartThreads + tid) < nk))
                 key[j] = DQDK_KEY_NONE;
-            if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
-                atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u);
+            const bool v = kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk;
+            const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
+            rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
         __syncthreads();
         wave0_excl_scan(lcnt, loff, kSubs, false);
         __syncthreads();
-        if (tid < kSubs)
-            lcnt[tid] = loff[tid];  // reused as the LDS stage cursor of each slice
         if (tid <= kSubs)
             a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
-        __syncthreads();
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
             if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
-                stage[atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u)] =
+                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         // the next item's keys load while this one is written out
         if (kP2Pipe && item + gridDim.x < nitems) {
