@@ -452,12 +452,10 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
-            // + part1's KEY_NONE run padding (kRunAlign > 1): at most kRunAlign - 1 per run
-            const size_t pad = (size_t)kL1Buckets * (kRunAlign - 1) * ((nk + kP1Chunk - 1) / kP1Chunk);
-            const size_t items = (nk + pad) / kPartChunk + kL1Buckets + 1;
+            const size_t items = nk / kPartChunk + kL1Buckets + 1;
             if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part1, (nk + pad + kStagePad) * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part2, (nk + pad + kStagePad) * 2)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part1, (nk + kStagePad) * 4)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part2, (nk + kStagePad) * 2)) != hipSuccess ||
                 (e = hipMalloc(&q->d_runs, items * kItemOffs * sizeof(uint16_t))) != hipSuccess ||
                 (e = hipMalloc(&q->d_hscratch, kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));

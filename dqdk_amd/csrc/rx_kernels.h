@@ -50,16 +50,15 @@ constexpr int kSliceThreads = 512;
 #ifndef DQDK_P1_KEYS
 #define DQDK_P1_KEYS 32
 #endif
-constexpr int kP1Threads = 1024;                            // part1 block size
+#ifndef DQDK_P1_THREADS
+#define DQDK_P1_THREADS 1024
+#endif
+constexpr int kP1Threads = DQDK_P1_THREADS;                 // part1 block size
 constexpr int kP1Keys = DQDK_P1_KEYS;                       // keys per thread
 constexpr int kP1Chunk = kP1Threads * kP1Keys;              // keys staged in LDS per block
-constexpr int kP1MinWaves = kP1Keys > 16 ? 4 : 8;           // waves per SIMD: 1 or 2 blocks per CU
-constexpr int kP1BlocksPerCu = kP1MinWaves / 4;
-#ifndef DQDK_RUN_ALIGN
-#define DQDK_RUN_ALIGN 1
-#endif
-constexpr uint32_t kRunAlign = DQDK_RUN_ALIGN;  // part1 runs padded with KEY_NONE to a multiple of this many keys
-constexpr uint32_t kBucketAlign = kRunAlign > 8 ? kRunAlign : 8;  // bucket starts in part1/part2 (16-B part2 stores)
+constexpr int kP1BlocksPerCu = kP1Chunk * 4 > 80 * 1024 ? 1 : 2;  // a 128-KB stage leaves room for one block
+constexpr int kP1MinWaves = kP1Threads / 64 * kP1BlocksPerCu / 4;  // waves per SIMD
+constexpr uint32_t kBucketAlign = 8;  // bucket starts in part1/part2 rounded to 8 keys (16-B part2 stores)
 constexpr uint32_t kStagePad = kL1Buckets * kBucketAlign;  // extra part1/part2 entries for that padding
 
 // u32 scratch words used by the partitioned histogram

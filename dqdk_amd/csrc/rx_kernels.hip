@@ -346,9 +346,6 @@ constexpr int kRingW = DQDK_RINGW;
 #ifndef DQDK_ST_AUX
 #define DQDK_ST_AUX 0
 #endif
-#ifndef DQDK_DEC_SINK
-#define DQDK_DEC_SINK 0
-#endif
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -378,12 +375,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
 }
 
 // LDS of one rx_decode block: partition bucket counts, per-frame out-of-bounds
-// counts and checksum sums (one slot per frame of each wave's tile), the
-// captured last checksum chunk of each frame, and a sink for lanes without
-// an event.  Frame slots are reset by their lane in phase C.
+// counts and checksum sums (one slot per frame of each wave's tile) and the
+// captured last checksum chunk of each frame.  Frame slots are reset by
+// their lane in phase C.
 constexpr int kLdsOob = 288;                      // [kWaves][64] out-of-bounds events per frame
-constexpr int kLdsSink = kLdsOob + kWaves * 64;   // lanes without an event count here
-constexpr int kLdsCnt = kLdsSink + 1;
+constexpr int kLdsCnt = kLdsOob + kWaves * 64;
 struct DecodeLds {
     uint32_t cnt[kLdsCnt];       // [0, kL1Buckets): keys per L1 bucket (partitioned histogram)
     uint32_t sum[kWaves * 64];   // checksum word sums per frame
@@ -457,15 +453,10 @@ __device__ __forceinline__ void decode_chunk(const u32x4& v, uint32_t r, uint32_
     const bool has = e < Ef;
     __builtin_amdgcn_raw_buffer_store_b32(key, keys_rsrc, has ? kbase + 4u * e : kOOB, 0, DQDK_ST_AUX);
     // KEY_NONE >> kL1Shift = 2047 > oob_slot > every bucket
-#if DQDK_DEC_SINK  // A/B only: lanes without an event count into one sink word
-    const uint32_t idx = has ? min(key >> kL1Shift, oob_slot) : (uint32_t)kLdsSink;
-    atomicAdd(&cnt[idx], 1u);
-#else
     // lanes without an event stay out of the LDS: at 1500 B 37 of a window's
     // 128 chunk slots carry none, and one shared sink word serialised them
     if (has)
         atomicAdd(&cnt[min(key >> kL1Shift, oob_slot)], 1u);
-#endif
 }
 
 // T = sum of the LE 16-bit words at even addresses of a chunk (chunk starts
@@ -864,7 +855,7 @@ __global__ void __launch_bounds__(256) rx_histo_atomic_kernel(HistoArgs a)
 // Exclusive scan of src[0..n) (n <= 320) into dst[0..n], dst[n] = total, by
 // wave 0 of the block (5 entries per lane).  Caller syncs afterwards.
 __device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* dst, int n, bool src_global,
-                                                uint32_t align = 1, uint32_t slack = 0)
+                                                uint32_t align = 1)
 {
     if (threadIdx.x >= 64)
         return;
@@ -873,7 +864,7 @@ __device__ __forceinline__ void wave0_excl_scan(const uint32_t* src, uint32_t* d
 #pragma unroll
     for (int j = 0; j < 5; j++) {
         const int i = lane * 5 + j;
-        v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) + slack : 0u;
+        v[j] = i < n ? (src_global ? __builtin_nontemporal_load(&src[i]) : src[i]) : 0u;
         v[j] = (v[j] + align - 1) & ~(align - 1);
         sum += v[j];
     }
@@ -943,9 +934,7 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
     constexpr int kOwn = (kL1Buckets + kP1Threads - 1) / kP1Threads;  // buckets reserved per thread (1)
-    // room for every chunk's KEY_NONE padding of every run
-    const uint32_t slack = (kRunAlign - 1) * ((total + kP1Chunk - 1) / kP1Chunk);
-    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign, slack);
+    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
     uint32_t key[kP1Keys];
     auto load = [&](uint32_t b0) {
         const uint32_t n0 = min(total - b0, (uint32_t)kP1Chunk);
@@ -979,8 +968,7 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
 #pragma unroll
         for (int o = 0; o < kOwn; o++) {
             const int b = tid + o * kP1Threads;
-            g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], (lcnt[b] + kRunAlign - 1) / kRunAlign * kRunAlign)
-                                             : 0u;
+            g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], lcnt[b]) : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kP1Keys; j++)
@@ -1002,15 +990,6 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
             const uint32_t k = stage[p];
             a.part1[p + gdel[k >> kL1Shift]] = k;
         }
-        if (kRunAlign > 1) {  // runs end on a kRunAlign boundary: no line is shared by two blocks' runs
-#pragma unroll
-            for (int o = 0; o < kOwn; o++) {
-                const int b = tid + o * kP1Threads;
-                if (b < kL1Buckets && lcnt[b])
-                    for (uint32_t p = off1[b] + g[o] + lcnt[b]; p % kRunAlign; p++)
-                        a.part1[p] = DQDK_KEY_NONE;
-            }
-        }
         __syncthreads();
     }
 }
@@ -1019,8 +998,7 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
 // (scan of ceil(bucket length / chunk)), once per batch.
 __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 {
-    const uint32_t slack = (kRunAlign - 1) * ((frames_limit(a) * a.E + kP1Chunk - 1) / kP1Chunk);  // as part1
-    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign, slack);
+    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign);
     const int lane = threadIdx.x;
     uint32_t v[5], sum = 0;
 #pragma unroll
@@ -1093,10 +1071,8 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         uint32_t rank[kPartKeysPerThread / 2];  // two u16 ranks per word (rank < kPartChunk)
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
-            // lanes past the chunk (and part1's KEY_NONE padding, kRunAlign > 1) are dropped
-            if (!((uint32_t)(j * kPartThreads + tid) < nk))
-                key[j] = DQDK_KEY_NONE;
-            const bool v = kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk;
+            // lanes past the chunk are dropped
+            const bool v = (uint32_t)(j * kPartThreads + tid) < nk;
             const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
             rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
@@ -1107,7 +1083,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
-            if (kRunAlign > 1 ? key[j] != DQDK_KEY_NONE : (uint32_t)(j * kPartThreads + tid) < nk)
+            if ((uint32_t)(j * kPartThreads + tid) < nk)
                 stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         // the next item's keys load while this one is written out
