@@ -64,7 +64,7 @@ MODE_WAVEFORM, MODE_LISTWAVE, MODE_LISTMODE, MODE_ENERGYHISTO = range(4)
 MODES = {"waveform": MODE_WAVEFORM, "listwave": MODE_LISTWAVE, "listmode": MODE_LISTMODE,
          "energy-histo": MODE_ENERGYHISTO}  # src/tristan.c:13-18
 F_CSUM, F_BATCH_ABORT, F_PREFILTER, F_NO_HISTO, F_CSUM_WRITEBACK = 1, 2, 4, 8, 16
-F_HISTO_ATOMIC, F_HISTO_PARTITIONED = 32, 64
+F_HISTO_ATOMIC, F_HISTO_PARTITIONED, F_HISTO_EAGER = 32, 64, 128
 KEY_NONE = 0xFFFFFFFF
 TIMING_STAGES = 9
 HISTO_CHANNELS, HISTO_HISTS, HISTO_BINS = 1512, 6, 65536
@@ -106,6 +106,7 @@ SIGNATURES = {
                                            C.c_int, C.POINTER(C.c_double)]),
     "dqdk_gpu_timing_enable": (C.c_int, [_P, C.c_int]),
     "dqdk_gpu_timing_stages": (C.c_int, [_P, C.c_uint32]),
+    "dqdk_gpu_histogram_flush": (C.c_int, [_P]),
     "dqdk_gpu_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     "dqdk_gpu_timing_stage_name": (C.c_char_p, [C.c_int]),
     "dqdk_gpu_last_error": (C.c_char_p, []),

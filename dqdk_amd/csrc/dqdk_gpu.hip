@@ -94,6 +94,13 @@ struct dqdk_gpu_queue {
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
+    // Partitioned batches stage their slice-sorted keys (part2 + runs +
+    // scratch, one slot each); the slice pass -- which sweeps the low-byte
+    // plane of every touched slice -- runs once over hist_k staged batches,
+    // and before anything reads the table (hist_flush).
+    uint32_t hist_k = 1;
+    uint32_t hist_pending = 0;
+    size_t part2_stride = 0, runs_stride = 0;  // elements per slot
     dqdk_gpu_desc_t* d_desc = nullptr;
     dqdk_gpu_rx_result_t* d_res = nullptr;
     // raw payload stream (tristan.c:318-324)
@@ -160,6 +167,34 @@ bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)
     return (uint64_t)n * q->E >= kPartitionMinKeys;
 }
 
+// The slice pass over every staged partitioned batch (see hist_k).
+int hist_flush(dqdk_gpu_queue* q)
+{
+    if (!q->hist_pending)
+        return 0;
+    HistoArgs ha{};
+    ha.hist = q->d_hist;
+    ha.lo = q->d_lo;
+    ha.scratch = q->d_hscratch;  // slot 0 also holds the heavy-slice list
+    ha.part2 = q->d_part2;
+    ha.runs = q->d_runs;
+    ha.nslots = q->hist_pending;
+    ha.scratch_stride = kHistScratchWords;
+    ha.part2_stride = q->part2_stride;
+    ha.runs_stride = q->runs_stride;
+    q->hist_pending = 0;
+    {
+        StageTimer t(q, kStSlice);
+        hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+    }
+    {
+        StageTimer t(q, kStHeavy);  // usually an empty list: exits at once
+        hipLaunchKernelGGL(rx_slice_heavy_kernel, dim3(q->cu_count), dim3(kSliceThreads), 0, q->stream, ha);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
 {
@@ -180,9 +215,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ra.port_end = q->cfg.port_end;
     ra.batch_scratch = q->d_batch;
     const bool partitioned = q->histo && q->E && use_partitioned(q, n);
-    ra.cnt1 = partitioned ? q->d_hscratch + kOffCnt1 : nullptr;
+    uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * kHistScratchWords;
+    ra.cnt1 = partitioned ? slot_scratch + kOffCnt1 : nullptr;
     if (partitioned)
-        HIPCHK(hipMemsetAsync(q->d_hscratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+        HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
     const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
@@ -225,10 +261,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.batch_scratch = q->d_batch;
         ha.hist = q->d_hist;
         ha.lo = q->d_lo;
-        ha.scratch = q->d_hscratch;
+        ha.scratch = slot_scratch;
         ha.part1 = q->d_part1;
-        ha.part2 = q->d_part2;
-        ha.runs = q->d_runs;
+        ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
+        ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
         if (!partitioned) {
             const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
             StageTimer t(q, kStAtomic);
@@ -251,14 +287,9 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
                 StageTimer t(q, kStPart2);
                 hipLaunchKernelGGL(rx_part2_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
             }
-            {
-                StageTimer t(q, kStSlice);
-                hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
-            }
-            {
-                StageTimer t(q, kStHeavy);  // usually an empty list: exits at once
-                hipLaunchKernelGGL(rx_slice_heavy_kernel, dim3(q->cu_count), dim3(kSliceThreads), 0, q->stream, ha);
-            }
+            HIPCHK(hipGetLastError());
+            if (++q->hist_pending == q->hist_k)
+                return hist_flush(q);
         }
         HIPCHK(hipGetLastError());
     }
@@ -453,11 +484,21 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
             const size_t items = nk / kPartChunk + kL1Buckets + 1;
+            // Stage up to 4 batches per slice pass while a full batch leaves
+            // each 16K-bin slice with fewer than ~4K events (so the low-byte
+            // sweep is amortised and a slice stays far below the 65535 events
+            // of the packed-u16 form); DQDK_GPU_F_HISTO_EAGER: every batch.
+            const size_t per_slice = (nk + kSlices - 1) / kSlices;
+            q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
+                            ? 1u
+                            : (uint32_t)std::max<size_t>(1, std::min<size_t>(4, 16384 / std::max<size_t>(per_slice, 1)));
+            q->part2_stride = nk + kStagePad;
+            q->runs_stride = items * kItemOffs;
             if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
                 (e = hipMalloc(&q->d_part1, (nk + kStagePad) * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part2, (nk + kStagePad) * 2)) != hipSuccess ||
-                (e = hipMalloc(&q->d_runs, items * kItemOffs * sizeof(uint16_t))) != hipSuccess ||
-                (e = hipMalloc(&q->d_hscratch, kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
+                (e = hipMalloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
+                (e = hipMalloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t))) != hipSuccess ||
+                (e = hipMalloc(&q->d_hscratch, q->hist_k * kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
         }
     }
@@ -641,6 +682,8 @@ int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_get: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
+    if (int rc = hist_flush(q))
+        return rc;
     return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
         memcpy(host_hist + o, h, m * sizeof(uint32_t));
     });
@@ -653,6 +696,8 @@ int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_accumulate: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
+    if (int rc = hist_flush(q))
+        return rc;
     return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
         for (uint64_t k = 0; k < m; k++)
             host_hist[o + k] += h[k];  // u32 wrap, like the shared atomic table
@@ -666,6 +711,7 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q)
     if (!q->d_hist)
         return 0;
     HIPCHK(hipSetDevice(q->device));
+    q->hist_pending = 0;  // staged batches are dropped with the table
     HIPCHK(hipMemsetAsync(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->stream));
     HIPCHK(hipMemsetAsync(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES, q->stream));
     return 0;
@@ -681,7 +727,8 @@ uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q)
         q->d_snap = nullptr;
         return nullptr;
     }
-    if (combine(q, q->d_snap, 0, DQDK_TRISTAN_HISTO_ENTRIES) != 0 || hipStreamSynchronize(q->stream) != hipSuccess)
+    if (hist_flush(q) != 0 || combine(q, q->d_snap, 0, DQDK_TRISTAN_HISTO_ENTRIES) != 0 ||
+        hipStreamSynchronize(q->stream) != hipSuccess)
         return nullptr;
     return q->d_snap;
 }
@@ -756,6 +803,16 @@ int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)
     return 0;
 }
 
+int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q)
+{
+    if (!q)
+        return -EINVAL;
+    if (!q->d_hist)
+        return 0;
+    HIPCHK(hipSetDevice(q->device));
+    return hist_flush(q);
+}
+
 int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst)
 {
     if (!q || !d_dst)
@@ -763,6 +820,8 @@ int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_copy: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
+    if (int rc = hist_flush(q))
+        return rc;
     return combine(q, d_dst, 0, DQDK_TRISTAN_HISTO_ENTRIES);
 }
 
@@ -786,6 +845,8 @@ int dqdk_gpu_histogram_nonzero(dqdk_gpu_queue_t* q, uint64_t* count)
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_nonzero: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
+    if (int rc = hist_flush(q))
+        return rc;
     unsigned long long* d = nullptr;
     HIPCHK(hipMalloc(&d, sizeof(*d)));
     hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), q->stream);
@@ -834,6 +895,8 @@ int dqdk_gpu_histogram_write_csv(dqdk_gpu_queue_t* q, int fd, uint64_t* bytes_wr
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_write_csv: queue has no histogram");
     HIPCHK(hipSetDevice(q->device));
+    if (int rc = hist_flush(q))
+        return rc;
     static const char header[] = "Channel,Histo,Energy,Freq\n";  // src/tristan.c:198
     int rc = write_all(fd, header, sizeof(header) - 1);
     if (rc)

@@ -110,6 +110,11 @@ struct HistoArgs {
     uint32_t* part1;    // n*E keys grouped by bucket
     uint16_t* part2;    // n*E slice-local keys (key & 16383), each 16K chunk of a bucket sorted by slice
     uint16_t* runs;     // [items][kItemOffs] slice run starts inside each chunk
+    // the slice pass runs over nslots staged batches: batch k's scratch,
+    // part2 keys and run offsets sit k strides (elements) after the first
+    uint32_t nslots;
+    uint32_t scratch_stride;
+    uint64_t part2_stride, runs_stride;
 };
 
 __global__ void rx_decode_kernel(RxArgs a);

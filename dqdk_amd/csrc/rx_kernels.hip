@@ -1137,26 +1137,34 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     const int lane = tid & 63, wave = tid >> 6;
     constexpr int kWavesS = kSliceThreads / 64;
     const uint32_t b = s / kSubs, sub = s % kSubs;
-    const uint32_t i0 = a.scratch[kOffIstart + b], i1 = a.scratch[kOffIstart + b + 1];
-    if (i0 == i1)
+    // staged batch k: its scratch (bucket starts, item starts), u16 keys, run offsets
+    auto sc = [&](uint32_t k) { return a.scratch + (uint64_t)k * a.scratch_stride; };
+    auto runs = [&](uint32_t k) { return a.runs + (uint64_t)k * a.runs_stride; };
+    bool any = false;
+    for (uint32_t k = 0; k < a.nslots; k++)
+        any |= sc(k)[kOffIstart + b] != sc(k)[kOffIstart + b + 1];
+    if (!any)
         return;
-    const uint32_t bstart = a.scratch[kOffOff1 + b];
     if (tid == 0)
         sl.total = 0;
     u32x4_t* h4 = (u32x4_t*)h;
     for (int c = tid; c < kWords / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
-    // events of this slice = sum of its run lengths; the first 512 items' runs stay in LDS
+    // events of this slice = sum of its run lengths over the staged batches;
+    // batch 0's first 512 items' runs stay in LDS
     uint32_t mine = 0;
-    for (uint32_t it = i0 + (uint32_t)tid; it < i1; it += kSliceThreads) {
-        const uint16_t* ro = a.runs + (uint64_t)it * kItemOffs + sub;
-        const uint32_t lo = ro[0], hi = ro[1];
-        if (it < i0 + kSliceThreads) {
-            sl.s_lo[tid] = lo;
-            sl.s_hi[tid] = hi;
+    for (uint32_t k = 0; k < a.nslots; k++) {
+        const uint32_t i0 = sc(k)[kOffIstart + b], i1 = sc(k)[kOffIstart + b + 1];
+        for (uint32_t it = i0 + (uint32_t)tid; it < i1; it += kSliceThreads) {
+            const uint16_t* ro = runs(k) + (uint64_t)it * kItemOffs + sub;
+            const uint32_t lo = ro[0], hi = ro[1];
+            if (k == 0 && it < i0 + kSliceThreads) {
+                sl.s_lo[tid] = lo;
+                sl.s_hi[tid] = hi;
+            }
+            mine += hi - lo;
         }
-        mine += hi - lo;
     }
     if (mine)
         atomicAdd(&sl.total, mine);
@@ -1188,12 +1196,16 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
 #endif
     constexpr int kNI = DQDK_SLICE_NI;
     constexpr int kKG = DQDK_SLICE_KG;
+    for (uint32_t k = 0; k < a.nslots; k++) {
+    const uint32_t i0 = sc(k)[kOffIstart + b], i1 = sc(k)[kOffIstart + b + 1];
+    const uint32_t bstart = sc(k)[kOffOff1 + b];
+    const uint16_t* part2 = a.part2 + (uint64_t)k * a.part2_stride;
     for (uint32_t ib = i0; ib < i1; ib += kSliceThreads) {
         const uint32_t nit = min(i1 - ib, (uint32_t)kSliceThreads);
-        if (ib != i0) {  // buckets with more than 512 items (skewed data)
+        if (k != 0 || ib != i0) {  // later batches; buckets with more than 512 items (skewed data)
             __syncthreads();
             if ((uint32_t)tid < nit) {
-                const uint16_t* ro = a.runs + (uint64_t)(ib + tid) * kItemOffs + sub;
+                const uint16_t* ro = runs(k) + (uint64_t)(ib + tid) * kItemOffs + sub;
                 sl.s_lo[tid] = ro[0];
                 sl.s_hi[tid] = ro[1];
             }
@@ -1211,7 +1223,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 dlo[q] = klo[q] >> 1;
                 dhi[q] = (khi[q] + 1) >> 1;
                 // item chunks start at multiples of kBucketAlign keys: dword-aligned
-                src[q] = (const uint32_t*)(a.part2 + bstart + (ib + jj - i0) * (uint32_t)kPartChunk);
+                src[q] = (const uint32_t*)(part2 + bstart + (ib + jj - i0) * (uint32_t)kPartChunk);
                 steps = max(steps, dhi[q] - dlo[q]);
             }
             for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
@@ -1236,6 +1248,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             }
         }
     }
+    }  // staged batch k
     __syncthreads();
     // low-byte plane: thread t owns bins [16t, 16t + 16) and [16(t + 512), +16)
 #pragma unroll

@@ -167,6 +167,10 @@ class RxQueue:
         assert into.dtype == np.uint32 and into.size == L.HISTO_ENTRIES and into.flags.c_contiguous
         L.check(L.lib().dqdk_gpu_histogram_accumulate(self._h, into.ctypes.data), "histogram_accumulate")
 
+    def flush_histogram(self) -> None:
+        """Run the pending slice pass of staged partitioned batches (async)."""
+        L.check(L.lib().dqdk_gpu_histogram_flush(self._h), "histogram_flush")
+
     def reset_histogram(self) -> None:
         L.check(L.lib().dqdk_gpu_histogram_reset(self._h), "histogram_reset")
 

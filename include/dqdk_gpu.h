@@ -103,6 +103,7 @@ enum dqdk_gpu_flags {
      * per batch by event count): */
     DQDK_GPU_F_HISTO_ATOMIC = 1u << 5,      /* one device atomic per event              */
     DQDK_GPU_F_HISTO_PARTITIONED = 1u << 6, /* bucket -> slice -> LDS histogram + RMW   */
+    DQDK_GPU_F_HISTO_EAGER = 1u << 7,       /* partitioned: slice pass after every batch */
 };
 
 typedef struct dqdk_gpu_cfg {
@@ -188,6 +189,13 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
  * buffer (synchronous) and returns it, valid until the next call or queue
  * destroy; NULL if the queue has no histogram. */
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
+/* Partitioned batches stage their slice-sorted events and the slice pass
+ * (the sweep of the table's low-byte plane) runs once per up to 4 staged
+ * batches when a batch leaves fewer than ~4K events per 16K-bin slice
+ * (DQDK_GPU_F_HISTO_EAGER: after every batch).  Every histogram reader
+ * above and below flushes first; flush runs the pending slice pass now
+ * (async on the queue stream). */
+int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q);
 
 /* ---- end-of-run egress (tristan_fini, src/tristan.c:162-233) ------------- */
 /* Merge helpers for per-GPU partial tables.  d_dst / d_src are device
