@@ -366,3 +366,40 @@ def test_auto_path_mixes_atomic_and_partitioned_batches_with_carries():
     nz = np.flatnonzero(hist)
     np.testing.assert_array_equal(nz, u)
     np.testing.assert_array_equal(hist[nz], c)
+
+
+def test_staged_slice_pass_flush_and_reset():
+    """Partitioned batches stage their events; the slice pass runs once per 4
+    staged batches and before any read.  Five batches (one automatic pass +
+    one pending at the read) sum like the oracle; reset drops the table with
+    whatever is staged; the next batch alone is then in the table."""
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
+    ref = []
+    with D.RxQueue(0, cfg, 1024) as q:
+        q.enable_timing(True)
+        for b in range(5):
+            umem, desc = D.synth_umem(1024, 1500, 4096, faulty=True, first=b * 1024)
+            run_gpu(umem, desc, cfg, keys=False, q=q)
+            r, _, k = O.rx_batch(umem.copy(), desc, 1458, flags=D.F_CSUM)
+            kk = k.reshape(-1, 91)[r["status"] == D.RX_OK].ravel()
+            ref.append(kk[kk != D.KEY_NONE])
+        assert q.read_timing()["rx_slice_histo"]["launches"] == 1  # after the 4th batch only
+        hist = q.histogram()
+        u, c = np.unique(np.concatenate(ref), return_counts=True)
+        nz = np.flatnonzero(hist)
+        np.testing.assert_array_equal(nz, u)
+        np.testing.assert_array_equal(hist[nz], c)
+        # staged batch, then reset: neither survives
+        umem, desc = D.synth_umem(1024, 1500, 4096, faulty=True, first=9000)
+        run_gpu(umem, desc, cfg, keys=False, q=q)
+        q.reset_histogram()
+        assert not q.histogram().any()
+        run_gpu(umem, desc, cfg, keys=False, q=q)
+        q.flush_histogram()
+        hist = q.histogram()
+    r, _, k = O.rx_batch(umem.copy(), desc, 1458, flags=D.F_CSUM)
+    u, c = O.sparse_histogram(k, r, 91)
+    nz = np.flatnonzero(hist)
+    np.testing.assert_array_equal(nz, u)
+    np.testing.assert_array_equal(hist[nz], c)
