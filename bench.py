@@ -155,9 +155,7 @@ def main():
         if name != "rx_decode":
             stages[name] = dict(s, batches=bd_steps)
     stages["rx_decode"]["batches"] = args.steps
-    # partitioned batches per slice pass (dqdk_gpu.hip queue_create: hist_k)
-    nk_slices = -(-(n * E) // 36352) if E else 1
-    hist_k = 1 if args.histo_eager else max(1, min(4, 16384 // max(1, nk_slices)))
+    hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass
 
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     step_median_ms = step_ms[len(step_ms) // 2]

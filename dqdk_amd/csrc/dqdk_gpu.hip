@@ -160,6 +160,15 @@ struct StageTimer {
 // each (measured, profiles/).  Partition once a batch carries enough events.
 constexpr uint64_t kPartitionMinKeys = 4u << 20;
 
+#ifndef DQDK_HIST_KMAX
+#define DQDK_HIST_KMAX 8
+#endif
+#ifndef DQDK_HIST_SLICE_EVENTS
+#define DQDK_HIST_SLICE_EVENTS 32768
+#endif
+constexpr size_t kHistKMax = DQDK_HIST_KMAX;                  // staged batches per slice pass, at most
+constexpr size_t kHistSliceEvents = DQDK_HIST_SLICE_EVENTS;  // staged events per slice, target
+
 bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)
 {
     if (q->histo_path)
@@ -484,14 +493,16 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
             const size_t items = nk / kPartChunk + kL1Buckets + 1;
-            // Stage up to 4 batches per slice pass while a full batch leaves
-            // each 16K-bin slice with fewer than ~4K events (so the low-byte
-            // sweep is amortised and a slice stays far below the 65535 events
-            // of the packed-u16 form); DQDK_GPU_F_HISTO_EAGER: every batch.
+            // Stage up to kHistKMax batches per slice pass, as many as keep a
+            // slice of uniformly spread events at half the 65535 events of the
+            // packed-u16 form (the low-byte sweep is amortised over them; a
+            // fuller slice still takes the u32 form); DQDK_GPU_F_HISTO_EAGER:
+            // a pass per batch.
             const size_t per_slice = (nk + kSlices - 1) / kSlices;
             q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
                             ? 1u
-                            : (uint32_t)std::max<size_t>(1, std::min<size_t>(4, 16384 / std::max<size_t>(per_slice, 1)));
+                            : (uint32_t)std::max<size_t>(
+                                  1, std::min<size_t>(kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1)));
             q->part2_stride = nk + kStagePad;
             q->runs_stride = items * kItemOffs;
             if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
@@ -802,6 +813,8 @@ int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)
     q->raw_fd = fd;
     return 0;
 }
+
+int dqdk_gpu_histogram_batches_per_pass(dqdk_gpu_queue_t* q) { return q ? (int)q->hist_k : -EINVAL; }
 
 int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q)
 {

@@ -171,6 +171,9 @@ class RxQueue:
         """Run the pending slice pass of staged partitioned batches (async)."""
         L.check(L.lib().dqdk_gpu_histogram_flush(self._h), "histogram_flush")
 
+    def histogram_batches_per_pass(self) -> int:
+        return int(L.lib().dqdk_gpu_histogram_batches_per_pass(self._h))
+
     def reset_histogram(self) -> None:
         L.check(L.lib().dqdk_gpu_histogram_reset(self._h), "histogram_reset")
 

@@ -190,12 +190,13 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
  * destroy; NULL if the queue has no histogram. */
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
 /* Partitioned batches stage their slice-sorted events and the slice pass
- * (the sweep of the table's low-byte plane) runs once per up to 4 staged
- * batches when a batch leaves fewer than ~4K events per 16K-bin slice
- * (DQDK_GPU_F_HISTO_EAGER: after every batch).  Every histogram reader
- * above and below flushes first; flush runs the pending slice pass now
- * (async on the queue stream). */
+ * (the sweep of the table's low-byte plane) runs once per
+ * batches_per_pass staged batches (up to 8, while a 16K-bin slice of
+ * uniformly spread events stays under 32K events; DQDK_GPU_F_HISTO_EAGER:
+ * 1).  Every histogram reader above and below flushes first; flush runs
+ * the pending slice pass now (async on the queue stream). */
 int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q);
+int dqdk_gpu_histogram_batches_per_pass(dqdk_gpu_queue_t* q);
 
 /* ---- end-of-run egress (tristan_fini, src/tristan.c:162-233) ------------- */
 /* Merge helpers for per-GPU partial tables.  d_dst / d_src are device

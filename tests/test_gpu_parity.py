@@ -369,8 +369,8 @@ def test_auto_path_mixes_atomic_and_partitioned_batches_with_carries():
 
 
 def test_staged_slice_pass_flush_and_reset():
-    """Partitioned batches stage their events; the slice pass runs once per 4
-    staged batches and before any read.  Five batches (one automatic pass +
+    """Partitioned batches stage their events; the slice pass runs once per k
+    staged batches and before any read.  k + 1 batches (one automatic pass +
     one pending at the read) sum like the oracle; reset drops the table with
     whatever is staged; the next batch alone is then in the table."""
     _need_gpu()
@@ -378,13 +378,15 @@ def test_staged_slice_pass_flush_and_reset():
     ref = []
     with D.RxQueue(0, cfg, 1024) as q:
         q.enable_timing(True)
-        for b in range(5):
+        kp = q.histogram_batches_per_pass()
+        assert kp > 1  # 1024 x 91 events: a few per slice
+        for b in range(kp + 1):
             umem, desc = D.synth_umem(1024, 1500, 4096, faulty=True, first=b * 1024)
             run_gpu(umem, desc, cfg, keys=False, q=q)
             r, _, k = O.rx_batch(umem.copy(), desc, 1458, flags=D.F_CSUM)
             kk = k.reshape(-1, 91)[r["status"] == D.RX_OK].ravel()
             ref.append(kk[kk != D.KEY_NONE])
-        assert q.read_timing()["rx_slice_histo"]["launches"] == 1  # after the 4th batch only
+        assert q.read_timing()["rx_slice_histo"]["launches"] == 1  # after the k-th batch only
         hist = q.histogram()
         u, c = np.unique(np.concatenate(ref), return_counts=True)
         nz = np.flatnonzero(hist)
