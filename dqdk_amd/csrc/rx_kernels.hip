@@ -1071,8 +1071,12 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         uint32_t rank[kPartKeysPerThread / 2];  // two u16 ranks per word (rank < kPartChunk)
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
-            // lanes past the chunk are dropped
+            // lanes past the chunk are dropped (and their key overwritten: the
+            // build without the overwrite ran 0.78 instead of 0.70 ms at 9000 B,
+            // with 29% more HBM reads by PMC; same load instructions)
             const bool v = (uint32_t)(j * kPartThreads + tid) < nk;
+            if (!v)
+                key[j] = DQDK_KEY_NONE;
             const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
             rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
