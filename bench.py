@@ -103,6 +103,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    q.flush_histogram()  # no warmup batch left staged for the timed region's slice passes
     torch.cuda.synchronize(dev)
     q.read_timing()  # discard
     # only rx_decode is bracketed by HIP events inside the timed region (the
