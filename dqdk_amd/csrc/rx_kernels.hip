@@ -962,14 +962,16 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
             rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
         __syncthreads();
-        wave0_excl_scan(lcnt, loff, kL1Buckets, false);
-        __syncthreads();
+        // the run reservations need only the counts: they go out before the
+        // scan, so their latency overlaps the scan, a barrier and the scatter
         uint32_t g[kOwn];
 #pragma unroll
         for (int o = 0; o < kOwn; o++) {
             const int b = tid + o * kP1Threads;
             g[o] = b < kL1Buckets && lcnt[b] ? atomicAdd(&cur1[b], lcnt[b]) : 0u;
         }
+        wave0_excl_scan(lcnt, loff, kL1Buckets, false);
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < kP1Keys; j++)
             if (key[j] != DQDK_KEY_NONE)
