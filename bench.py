@@ -11,7 +11,11 @@ histogram_event, src/tristan.c:233-330) + the fetch_xsk counters
 Default workload (BASELINE.json configs[1] frame size with the metric's full
 parse + decode path, north-star batch size): 1,048,576 x 1500 B synthetic
 UDP frames at the UMEM-faithful 4096 B stride, payloadsz 1458 (E = 91).
-`--frame-len 9000 --stride 9216` gives the jumbo-frame config (configs[2]).
+`--frame-len 9000 --stride 9216` gives the jumbo-frame config (configs[2]);
+`--frames 262144 --no-histo --no-records` is configs[1]'s parse + checksum
+only; `--frame-len 0` the mixed config (configs[3]): each frame 1500 or 9000 B by a
+seeded coin flip (synth.c), stride 9216, payloadsz 1458 (the reference's E
+comes from the configured payload size, not the frame, tristan.c:311).
 
 Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one RX queue per
 GPU, each rank its own frames and histogram, no collective in the data path
@@ -43,7 +47,7 @@ def parse_args():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--frames", type=int, default=1 << 20)
-    p.add_argument("--frame-len", type=int, default=1500)
+    p.add_argument("--frame-len", type=int, default=1500, help="0 = mixed 1500/9000 B (configs[3])")
     p.add_argument("--stride", type=int, default=0, help="UMEM slot bytes (default 4096, or 9216 for > 4096 B)")
     p.add_argument("--payloadsz", type=int, default=0, help="-s; default frame_len - 42")
     p.add_argument("--mode", default="energy-histo")
@@ -76,8 +80,9 @@ def main():
     torch.cuda.set_device(dev)
 
     L = args.frame_len
-    stride = args.stride or (4096 if L <= 4096 else 9216)
-    payloadsz = args.payloadsz or max(L - 42, 0)
+    mixed = L == 0
+    stride = args.stride or (4096 if 0 < L <= 4096 else 9216)
+    payloadsz = args.payloadsz or (1458 if mixed else max(L - 42, 0))
     n = args.frames
     flags = (0 if args.no_csum else D.F_CSUM) | (D.F_NO_HISTO if args.no_histo else 0) | \
         (D.F_HISTO_EAGER if args.histo_eager else 0)
@@ -93,6 +98,8 @@ def main():
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
     umem_bytes = umem.nbytes
+    frame_bytes = int(desc["len"].astype(np.int64).sum())  # per batch (n * L unless mixed)
+    Lm = frame_bytes / n  # mean frame length
     q = D.RxQueue(local, cfg, n)
     stream = torch.cuda.current_stream(dev)
     q.set_stream(stream.cuda_stream)
@@ -162,10 +169,11 @@ def main():
     step_median_ms = step_ms[len(step_ms) // 2]
     total_pkts = n * args.steps * world
     mpkts = total_pkts / elapsed / 1e6
-    frame_gbs = total_pkts * L / elapsed / 1e9
+    frame_gbs = total_pkts * Lm / elapsed / 1e9
 
     # ---- per-kernel algorithmic bytes per launch ------------
     K = n * E  # decoded records per batch
+    keys_written = histo or not args.no_records
     items = K // (1 << 14) + 284 + 1  # part2 work items (16K-key chunks of the 284 buckets)
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
@@ -174,7 +182,8 @@ def main():
         touched = int(torch.unique(kk[kk >= 0] >> 14).numel())  # 16K-bin slices with >= 1 event
     alg = {
         # the metric's path: desc + frame (the UDP checksum reads all of it) + result + 4-B record per event
-        "rx_decode": n * (16 + L + 8) + 4 * K,
+        # (no records and no histogram: parse + checksum only, configs[1] -- nothing written per event)
+        "rx_decode": n * (16 + 8) + frame_bytes + (4 * K if keys_written else 0),
         "rx_abort": 8 * n,
         "rx_count": 8 * n,
         "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
@@ -217,7 +226,7 @@ def main():
     stream_gbs = umem_bytes // 16 * 16 / (ms.value * 1e-3) / 1e9
     # the same frames read as rx_decode reads them (one wave per frame) and
     # 4 B per event written: the pattern's practical rate without arithmetic
-    fbytes = (L + 15) // 16 * 16
+    fbytes = (round(Lm) + 15) // 16 * 16  # mixed: every frame read at the mean length
     pattern = {}
     for name, flat, out in (("per_frame", 0, True), ("per_frame_read_only", 0, False), ("flat", 1, True),
                             ("flat_read_only", 1, False)):
@@ -262,7 +271,8 @@ def main():
     roofline = {"bound": "hbm", "kernel": "rx_decode",
                 "achieved": dec.get("GB_s"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dec.get("frac_hbm"), "traffic": traffic,
-                "alg_bytes_per_frame": 16 + L + 8 + 4 * E, "frames_per_launch": n,
+                "alg_bytes_per_frame": round(16 + Lm + 8 + (4 * E if keys_written else 0), 1),
+                "frames_per_launch": n,
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
                 "measured_frames_pattern_GB_s": pattern,
@@ -288,10 +298,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 TRISTAN-over-UDP frames, SURVEY §8(d))",
-            "config": {"workload": f"{n} x {L} B UDP frames (stride {stride}) parse+"
+            "config": {"workload": f"{n} x {'mixed 1500/9000' if mixed else L} B UDP frames (stride {stride}) parse+"
                                    f"{'' if args.no_csum else 'ip/udp checksum+'}TRISTAN {args.mode} decode"
+                                   f"{'' if keys_written else ' (OOB counts only, no records written)'}"
                                    f"{'+histogram' if histo else ''}, device-resident",
-                       "frames_per_batch": n, "frame_len": L, "stride": stride, "payloadsz": payloadsz,
+                       "frames_per_batch": n, "frame_len": "mixed 1500/9000" if mixed else L,
+                       "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
                        "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
                        "parallelism": f"queue-per-gpu x{world}"},
             "frame_GB_s": round(frame_gbs, 2),
