@@ -161,7 +161,7 @@ struct StageTimer {
 constexpr uint64_t kPartitionMinKeys = 4u << 20;
 
 #ifndef DQDK_HIST_KMAX
-#define DQDK_HIST_KMAX 8
+#define DQDK_HIST_KMAX 12
 #endif
 #ifndef DQDK_HIST_SLICE_EVENTS
 #define DQDK_HIST_SLICE_EVENTS 32768
