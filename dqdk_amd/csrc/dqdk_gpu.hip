@@ -231,7 +231,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
 
     const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
-#define DQDK_DEC_BLOCKS_PER_CU 8u
+#define DQDK_DEC_BLOCKS_PER_CU 16u
 #endif
     const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * DQDK_DEC_BLOCKS_PER_CU);
     {
