@@ -8,19 +8,25 @@ event into the queue's 2.38 GB histogram (tristan_process /
 histogram_event, src/tristan.c:233-330) + the fetch_xsk counters
 (src/dqdk.c:252-322).  Frames are resident in HBM before the timed region.
 
-Default workload (BASELINE.json configs[1] frame size with the metric's full
-parse + decode path, north-star batch size): 1,048,576 x 1500 B synthetic
-UDP frames at the UMEM-faithful 4096 B stride, payloadsz 1458 (E = 91).
-`--frame-len 9000 --stride 9216` gives the jumbo-frame config (configs[2]);
-`--frames 262144 --no-histo --no-records` is configs[1]'s parse + checksum
-only; `--frame-len 0` the mixed config (configs[3]): each frame 1500 or 9000 B by a
-seeded coin flip (synth.c), stride 9216, payloadsz 1458 (the reference's E
-comes from the configured payload size, not the frame, tristan.c:311).
+Default run (BASELINE.json metric "..., 1500B & 9000B"): the headline
+`value` is 1,048,576 x 1500 B synthetic UDP frames at the UMEM-faithful
+4096 B stride, payloadsz 1458 (E = 91), and the same JSON line carries the
+north-star's second size under `by_frame_len["9000"]`: 1,048,576 x 9000 B at
+stride 9216 (payloadsz 8958, E = 559), measured the same way (its own
+kernels, roofline and CPU baseline).  Other BASELINE configs:
 
-Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one RX queue per
-GPU, each rank its own frames and histogram, no collective in the data path
-(SURVEY §8(e)); barrier + max-over-ranks timing; value = all ranks' packets
-/ max time ("scaling": "weak").
+  configs[1]  --frames 262144 --no-histo --no-records   parse + checksum only
+  configs[2]  --frame-len 9000 --frames 262144           jumbo, full path
+  configs[3]  --gpus 4 --frame-len 0                     4 queues, 1500/9000 mix
+  configs[4]  --gpus 8 --e2e                             PCIe-inclusive replay,
+              pinned H2D / D2H on side streams, paced at --offered-gbps
+              (100 Gbit/s over all queues) plus the unpaced maximum
+
+Multi-GPU: one RX queue per GPU, each rank its own frames and histogram, no
+collective on the data path; barrier + max-over-ranks
+timing; value = all ranks' packets / max time ("scaling": "weak").  Under
+torchrun (WORLD_SIZE set) the ranks come from the environment; otherwise
+`--gpus N` starts N fresh child ranks itself (before any HIP call here).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -29,6 +35,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -39,9 +47,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Mpkt/s & GB/s device-resident UDP/IP parse+TRISTAN decode, 1500B & 9000B"
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -55,31 +64,81 @@ def parse_args():
     p.add_argument("--no-histo", action="store_true", help="decode only (no histogram accumulation)")
     p.add_argument("--histo-eager", action="store_true", help="slice pass after every batch (no staging)")
     p.add_argument("--no-records", action="store_true",
-                   help="diagnostic: with --no-histo, pass no record buffer (decode writes nothing)")
-    p.add_argument("--cpu-baseline-sec", type=float, default=10.0)
+                   help="with --no-histo: pass no record buffer (parse + checksum only, configs[1])")
+    p.add_argument("--no-9000", action="store_true", help="default run: skip the by_frame_len 9000 B measurement")
+    p.add_argument("--e2e", action="store_true", help="PCIe-inclusive pipeline (configs[4])")
+    p.add_argument("--e2e-frames", type=int, default=1 << 16, help="frames per e2e batch")
+    p.add_argument("--offered-gbps", type=float, default=100.0, help="e2e offered load over all queues (Gbit/s)")
+    p.add_argument("--cpu-baseline-sec", type=float, default=8.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_summary.json"),
                    help="rocprofv3 PMC summary used for roofline.traffic")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def main():
-    args = parse_args()
-    import torch
-    import torch.distributed as dist
+# ---- rank launch -------------------------------------------------------------
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without torchrun: N fresh child processes, one per GPU, with
+    the torchrun environment (this process never touches HIP).  Returns the
+    first non-zero child exit code, else 0."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for o in alive:  # one rank failed: the collective would hang the others
+                    o.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---- one workload ----------------------------------------------------------------
+
+def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16):
+    """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
+    (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample)."""
+    import dqdk_amd._lib as LIB
+    c = D.rx.synth_cfg(L, stride, queue)
+    size = int(LIB.lib().dqdk_synth_umem_size(__import__("ctypes").byref(c), n))
+    size = (size + 15) // 16 * 16
+    d_umem = torch.empty(size, dtype=torch.uint8, device=dev)
+    descs = []
+    sample = None
+    for f0 in range(0, n, chunk):
+        m = min(chunk, n - f0)
+        u, d = D.synth_umem(m, L, stride, queue=queue, first=f0, threads=16)
+        d = d.copy()
+        d["addr"] += f0 * stride
+        d_umem[f0 * stride:f0 * stride + u.size].copy_(torch.from_numpy(u))
+        descs.append(d)
+        if sample is None:
+            sample = (u, d.copy())  # the CPU baseline's sample: the workload's first frames
+    desc = np.concatenate(descs)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    return d_umem, d_desc, desc, sample
+
+
+def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
+    import ctypes as C
 
     import dqdk_amd as D
+    from dqdk_amd import _lib as LIB
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    L = args.frame_len
     mixed = L == 0
     stride = args.stride or (4096 if 0 < L <= 4096 else 9216)
     payloadsz = args.payloadsz or (1458 if mixed else max(L - 42, 0))
@@ -90,14 +149,13 @@ def main():
     cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags)
     E = cfg.events
     histo = D.histo_enabled(mode, flags)
+    keys_written = histo or not args.no_records
 
     # ---- input: queue `rank` of the synthetic UMEM replay, resident in HBM ----
-    umem, desc = D.synth_umem(n, L, stride, queue=rank, threads=16)
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_umem, d_desc, desc, sample = synth_to_device(D, torch, dev, n, L, stride, queue=rank)
+    umem_bytes = d_umem.numel()
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
-    umem_bytes = umem.nbytes
     frame_bytes = int(desc["len"].astype(np.int64).sum())  # per batch (n * L unless mixed)
     Lm = frame_bytes / n  # mean frame length
     q = D.RxQueue(local, cfg, n)
@@ -131,16 +189,14 @@ def main():
     # one runs inside the timed region, so every timed batch is in the table
     q.flush_histogram()
     torch.cuda.synchronize(dev)
+    t_rank = time.perf_counter() - t0  # this rank's own time (per-GPU rate)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     q.enable_timing(False)
     stages = q.read_timing()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, per_rank = aggregate_ranks(torch, dist, dev, world, t1 - t0, t_rank, n * args.steps,
+                                        frame_bytes * args.steps)
 
     # correctness guard on the measured batch (cheap, outside the timed region)
     cnt = q.counters()
@@ -166,14 +222,12 @@ def main():
     hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass
 
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
-    step_median_ms = step_ms[len(step_ms) // 2]
     total_pkts = n * args.steps * world
     mpkts = total_pkts / elapsed / 1e6
-    frame_gbs = total_pkts * Lm / elapsed / 1e9
+    frame_gbs = frame_bytes * args.steps * world / elapsed / 1e9
 
     # ---- per-kernel algorithmic bytes per launch ------------
     K = n * E  # decoded records per batch
-    keys_written = histo or not args.no_records
     items = K // (1 << 14) + 284 + 1  # part2 work items (16K-key chunks of the 284 buckets)
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
@@ -187,14 +241,13 @@ def main():
         "rx_abort": 8 * n,
         "rx_count": 8 * n,
         "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
-        "rx_part1": 8 * K,  # keys read + bucket runs written (+ two 1.1 KB count rows per unit)
-        # count scan: the decode's per-tile bucket-count rows prefixed in place, group rows summed twice
-        "rx_hist_prep": 8 * 288 * (-(-n // 64)) + 12 * 288 * (-(-n // 4096)),
+        "rx_part1": 8 * K,  # keys read + bucket runs written
+        "rx_hist_prep": 12 * 288,
         "rx_part2": 6 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
         # (per batch: one slice pass sweeps for hist_k staged batches)
-        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14) // hist_k,
+        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14) // max(hist_k, 1),
         "rx_slice_heavy": 0,  # slices redone with u32 bins (none at uniform spectra); bytes counted above
     }
     st = {}
@@ -202,18 +255,13 @@ def main():
         if s["launches"]:
             avg_ms = s["ms"] / s["launches"]
             batch_ms = s["ms"] / s["batches"]  # the slice kernels launch once per hist_k batches
-            gbs = alg[name] / (batch_ms * 1e-3) / 1e9
+            gbs = alg.get(name, 0) / (batch_ms * 1e-3) / 1e9
             st[name] = {"avg_ms": round(avg_ms, 4), "launches": s["launches"], "ms_per_batch": round(batch_ms, 4),
-                        "alg_bytes": alg[name], "GB_s": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+                        "alg_bytes": alg.get(name, 0), "GB_s": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
 
     # measured bounds on this GPU (membench.hip): streaming read over the UMEM
     # image, random u32 atomics of the same records into a scratch table
-    import ctypes as C
-
-    from dqdk_amd import _lib as LIB
     ms = C.c_double()
-    # random-atomic bound of the histogram, on this batch's records (before the
-    # pattern benchmarks below reuse the records buffer as their sink)
     atomic_gupd = None
     if histo and E:
         scratch = torch.zeros(D.HISTO_ENTRIES, dtype=torch.int32, device=dev)
@@ -224,42 +272,30 @@ def main():
     LIB.check(LIB.lib().dqdk_gpu_membench_read(d_umem.data_ptr(), umem_bytes // 16 * 16, stream.cuda_stream, 5,
                                                C.byref(ms)), "membench_read")
     stream_gbs = umem_bytes // 16 * 16 / (ms.value * 1e-3) / 1e9
-    # the same frames read as rx_decode reads them (one wave per frame) and
-    # 4 B per event written: the pattern's practical rate without arithmetic
+    # the same frames read one wave per frame with 4 B per event written: the
+    # pattern's practical rate without arithmetic
     fbytes = (round(Lm) + 15) // 16 * 16  # mixed: every frame read at the mean length
     pattern = {}
-    for name, flat, out in (("per_frame", 0, True), ("per_frame_read_only", 0, False), ("flat", 1, True),
-                            ("flat_read_only", 1, False)):
-        LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, fbytes, n,
-                                                     d_keys.data_ptr() if (E and out) else None, 4 * E if out else 0,
-                                                     flat, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
-        pattern[name] = round(n * (fbytes + (4 * E if out else 0)) / (ms.value * 1e-3) / 1e9, 1)
-    # contiguous 4:1 read:write copy over the same bytes (no frames): records buffer as the sink
-    mix_n = min(n, d_keys.numel() * 4 // stride)
-    LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, stride, mix_n, d_keys.data_ptr(), 0, 3,
-                                                 stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
-    pattern["contiguous_mix_4to1"] = round(mix_n * stride * 1.25 / (ms.value * 1e-3) / 1e9, 1)
-    cp_n = min(n, d_keys.numel() * 4 // stride)
-    LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, stride, cp_n, d_keys.data_ptr(), 0, 4,
-                                                 stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
-    pattern["contiguous_copy_1to1"] = round(cp_n * stride * 2 / (ms.value * 1e-3) / 1e9, 1)
-    pattern_gbs = pattern["per_frame"]
+    if E:
+        LIB.check(LIB.lib().dqdk_gpu_membench_frames(d_umem.data_ptr(), stride, fbytes, n, d_keys.data_ptr(), 4 * E,
+                                                     0, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
+        pattern["per_frame"] = round(n * (fbytes + 4 * E) / (ms.value * 1e-3) / 1e9, 1)
 
     hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo",
                                 "rx_slice_heavy") if k in st]
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["ms_per_batch"] for k in hist_kernels)
+        h_bytes = sum(alg[k] for k in hist_kernels if k != "rx_histo_atomic")
         gupd = K / (h_ms * 1e-3) / 1e9
         histogram = {"kernels": hist_kernels, "updates_per_batch": K, "touched_slices": touched,
                      "batches_per_slice_pass": hist_k if "rx_slice_histo" in st else None,
                      "ms": round(h_ms, 4), "Gupd_s": round(gupd, 2),
-                     "bound": {"kind": "random u32 atomic increment, measured on these records "
-                                       "(dqdk_gpu_membench_atomic)", "Gupd_s": round(atomic_gupd, 2)},
-                     "vs_bound": round(gupd / atomic_gupd, 3)}
+                     # the partitioned chain streams its staging (bytes above) once per batch: its roofline
+                     "streamed_bytes": h_bytes, "streamed_GB_s": round(h_bytes / (h_ms * 1e-3) / 1e9, 1),
+                     "frac_hbm": round(h_bytes / (h_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "random_atomic_Gupd_s": round(atomic_gupd, 2) if atomic_gupd else None}
 
-    # ---- roofline: rx_decode, the kernel §8(d)'s per-packet bytes price -----
-    dom = max(st, key=lambda k: st[k]["avg_ms"]) if st else "rx_decode"
     traffic = None
     try:
         pmc = json.loads(Path(args.pmc).read_text())
@@ -275,90 +311,219 @@ def main():
                 "frames_per_launch": n,
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
-                "measured_frames_pattern_GB_s": pattern,
-                "frac_of_measured_pattern": round(dec["GB_s"] / pattern_gbs, 4) if dec else None,
-                "slowest_kernel": dom}
+                "measured_frames_pattern_GB_s": pattern}
 
-    # ---- CPU baseline: the oracle (C restatement) on rank 0 at N=1 ----------
+    # ---- CPU baseline: the oracle (C restatement), rank 0, outside the timed region ----
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(umem, desc, cfg, histo, args.cpu_baseline_sec)
-
-    if rank == 0:
-        line = {
-            "metric": "Mpkt/s & GB/s device-resident UDP/IP parse+TRISTAN decode, 1500B & 9000B",
-            "value": round(mpkts, 3),
-            "unit": "Mpkt/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded splitmix64 TRISTAN-over-UDP frames, SURVEY §8(d))",
-            "config": {"workload": f"{n} x {'mixed 1500/9000' if mixed else L} B UDP frames (stride {stride}) parse+"
-                                   f"{'' if args.no_csum else 'ip/udp checksum+'}TRISTAN {args.mode} decode"
-                                   f"{'' if keys_written else ' (OOB counts only, no records written)'}"
-                                   f"{'+histogram' if histo else ''}, device-resident",
-                       "frames_per_batch": n, "frame_len": "mixed 1500/9000" if mixed else L,
-                       "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
-                       "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
-                       "parallelism": f"queue-per-gpu x{world}"},
-            "frame_GB_s": round(frame_gbs, 2),
-            "step_ms_median": round(step_median_ms, 4),
-            "step_ms_min": round(step_ms[0], 4),
-            "kernels": st,
-            "kernels_timing": "rx_decode: HIP events on the queue stream over the timed steps (the only kernel "
-                              "bracketed there); the others: HIP events over a separate pass of "
-                              f"{bd_steps} steps with every launch bracketed; ms_per_batch = kernel time / batches "
-                              "(the slice kernels run once per batches_per_slice_pass staged batches)",
-            "histogram": histogram,
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    q.close()
+    if rank == 0 and cpu_sec > 0:
+        cpu = cpu_baseline(sample, cfg, histo, cpu_sec, world)
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+
+    q.close()
+    del d_umem, d_desc, d_res, d_keys
+    torch.cuda.empty_cache()
+    return {
+        "value": round(mpkts, 3), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "config": {"workload": f"{n} x {'mixed 1500/9000' if mixed else L} B UDP frames (stride {stride}) parse+"
+                               f"{'' if args.no_csum else 'ip/udp checksum+'}TRISTAN {args.mode} decode"
+                               f"{'' if keys_written else ' (no event work: no records, no histogram)'}"
+                               f"{'+histogram' if histo else ''}, device-resident",
+                   "frames_per_batch": n, "frame_len": "mixed 1500/9000" if mixed else L,
+                   "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
+                   "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
+                   "parallelism": f"queue-per-gpu x{world}"},
+        "frame_GB_s": round(frame_gbs, 2),
+        "per_gpu": per_rank,
+        "step_ms_median": round(step_ms[len(step_ms) // 2], 4),
+        "step_ms_min": round(step_ms[0], 4),
+        "kernels": st,
+        "histogram": histogram,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
 
 
-def cpu_baseline(umem, desc, cfg, histo, budget_sec):
+def aggregate_ranks(torch, dist, dev, world, elapsed, t_rank, packets, frame_bytes):
+    """Job time = max over ranks of the barrier-bracketed time; per-GPU rates
+    from each rank's own time.  Returns (elapsed, per_gpu list or None)."""
+    if world == 1:
+        return elapsed, None
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    mine = torch.tensor([packets / t_rank / 1e6, frame_bytes / t_rank / 1e9], dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    return float(t.item()), [{"rank": r, "Mpkt_s": round(float(v[0]), 3), "frame_GB_s": round(float(v[1]), 2)}
+                             for r, v in enumerate(allr)]
+
+
+def dry_run(args, torch, dist, dev, rank, world):
+    """--cpu-dry-run: the launch / barrier / max-over-ranks / line path with
+    gloo on CPU and no GPU work (each rank sleeps a rank-dependent time per
+    step); exercised by tests/test_bench_launch.py."""
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.02 * (1 + rank))
+    t_rank = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed, per_rank = aggregate_ranks(torch, dist, dev, world, time.perf_counter() - t0, t_rank,
+                                        args.frames * args.steps, args.frames * 1500 * args.steps)
+    return {"value": round(args.frames * args.steps * world / elapsed / 1e6, 3),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "per_gpu": per_rank,
+            "config": {"workload": "dry run (no GPU work)", "parallelism": f"queue-per-gpu x{world}"}}
+
+
+def cpu_baseline(sample, cfg, histo, budget_sec, world):
     """Oracle (C restatement of src/tcpip + get_udp_payload + tristan_process)
-    on one host core: the reference's one worker pthread per queue.  Bounded
-    sample: the workload's first 65,536 frames, repeated until ~budget_sec."""
-    import os as _os
-
+    on the host cores: the reference's one worker pthread per queue sharing one
+    table through relaxed atomics (src/dqdk.c:517-620, src/tristan.c:243).
+    Bounded sample: the workload's first 65,536 frames (host copy), 1 thread
+    repeated for ~budget_sec, then 2/4/8 threads splitting the same frames."""
     from oracle import oracle as O
-    sample = min(len(desc), 65536)
-    sub = desc[:sample]
+    umem, desc = sample
     hist = np.zeros(O.HISTO_ENTRIES, dtype=np.uint32) if histo else None
     if hist is not None:
         hist[:] = 0  # pre-fault the 2.38 GB table (the reference uses hugepages, tristan.c:136-139)
-    passes, sec = 0, 0.0
-    while sec < budget_sec and passes < 1000:
-        s, _ = O.rx_batch_threads(umem, sub, cfg.payloadsz, cfg.mode, cfg.flags, hist, threads=1)
-        sec += s
-        passes += 1
-    rate = sample * passes / sec / 1e6
-    # one pinned worker per queue is the reference's model (src/dqdk.c:517-620):
-    # 2/4/8 workers on 2/4/8 x the sample, sharing the table (relaxed atomics)
-    threads = {}
+
+    def rate(threads, sec):
+        passes, t = 0, 0.0
+        while t < sec and passes < 1000:
+            s, _ = O.rx_batch_threads(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, hist, threads=threads)
+            t += s
+            passes += 1
+        return len(desc) * passes / t / 1e6, passes, t
+
+    r1, passes, sec = rate(1, budget_sec)
+    threads = {"1": round(r1, 4)}
     for t in (2, 4, 8):
-        m = min(len(desc), t * sample)
-        st, _ = O.rx_batch_threads(umem, desc[:m], cfg.payloadsz, cfg.mode, cfg.flags, hist, threads=t)
-        threads[str(t)] = round(m / st / 1e6, 4)
+        threads[str(t)] = round(rate(t, min(2.0, budget_sec))[0], 4)
     model = ""
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         pass
-    return {"value": round(rate, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} frames of the workload x {passes} passes ({sec:.1f} s), "
-                      f"1 thread, histogram {'on (2.38 GB table)' if histo else 'off'}; "
-                      f"host {model}, nproc {_os.cpu_count()}",
+    # one worker thread per queue: the N-queue comparison is N threads
+    t_match = str(min(world, 8)) if str(min(world, 8)) in threads else "1"
+    return {"value": threads[t_match], "unit": "Mpkt/s", "cores": int(t_match), "kind": "port",
+            "sample": f"first {len(desc)} frames of the workload; 1 thread x {passes} passes ({sec:.1f} s); "
+                      f"2/4/8 threads split the same frames; histogram {'on (2.38 GB table)' if histo else 'off'}; "
+                      f"host {model}, nproc {os.cpu_count()}",
             "threads_Mpkt_s": threads}
+
+
+# ---- PCIe-inclusive replay (configs[4]) --------------------------------------------
+
+def run_e2e(args, torch, dist, dev, rank, world, local):
+    import dqdk_amd as D
+    from dqdk_amd.pipeline import E2EPipeline
+
+    L = args.frame_len
+    stride = args.stride or (4096 if 0 < L <= 4096 else 9216)
+    payloadsz = args.payloadsz or (1458 if L == 0 else L - 42)
+    cfg = D.RxConfig(payloadsz=payloadsz, mode=D.MODES[args.mode], flags=0 if args.no_csum else D.F_CSUM)
+    n = args.e2e_frames
+    pl = E2EPipeline(local, cfg, n, L, stride, queue=rank, depth=3, images=2)
+    pl.run(3)  # warm-up
+    out = {}
+    for name, rate in (("unpaced", None), ("paced", args.offered_gbps * 1e9 / 8 / world)):
+        if world > 1:
+            dist.barrier()
+        r = pl.run(args.steps, rate)
+        t = torch.tensor([r["sec"], r["Mpkt_s"], r["batch_latency_ms"]["p99"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            allr = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(allr, t)
+        else:
+            allr = [t]
+        sec = max(float(a[0]) for a in allr)
+        out[name] = {"Mpkt_s": round(r["packets"] * world / sec / 1e6, 3),
+                     "frame_GB_s": round(pl.frame_bytes * args.steps * world / sec / 1e9, 2),
+                     "per_gpu_Mpkt_s": [round(float(a[1]), 3) for a in allr],
+                     "pcie_h2d_GB_s_per_gpu": round(r["pcie_h2d_GB_s"], 2),
+                     "pcie_d2h_GB_s_per_gpu": round(r["pcie_d2h_GB_s"], 3),
+                     "batch_latency_ms_p99_max": round(max(float(a[2]) for a in allr), 3),
+                     "batch_latency_ms_rank0": {k: round(v, 3) for k, v in r["batch_latency_ms"].items()}}
+        if rate:
+            out[name]["offered_Gbit_s"] = args.offered_gbps
+            out[name]["offered_Mpkt_s"] = round(args.offered_gbps * 1e9 / 8 / (pl.frame_bytes / n) / 1e6, 3)
+    pl.close()
+    return {
+        "value": out["unpaced"]["Mpkt_s"], "ms_per_step": round(out["unpaced"]["frame_GB_s"] and
+                                                                (pl.frame_bytes * world / (out["unpaced"]["frame_GB_s"] * 1e9)) * 1e3, 4),
+        "config": {"workload": f"{world} queue(s) x {n} x {L or 'mixed 1500/9000'} B frames per batch, end-to-end: "
+                               "pinned host UMEM -> H2D (side stream) -> parse+checksum+decode+histogram -> D2H "
+                               "results (side stream), PCIe-inclusive", "frames_per_batch": n, "frame_len": L,
+                   "stride": stride, "payloadsz": payloadsz, "parallelism": f"queue-per-gpu x{world}"},
+        "e2e": out,
+    }
+
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # before any HIP call in this process
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    if args.cpu_dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    if world > 1:
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+
+    cpu_sec = 0.0 if args.no_cpu_baseline else args.cpu_baseline_sec
+    extra = {}
+    if args.cpu_dry_run:
+        r = dry_run(args, torch, dist, dev, rank, world)
+    elif args.e2e:
+        r = run_e2e(args, torch, dist, dev, rank, world, local)
+    else:
+        r = measure(args, args.frame_len, torch, dist, dev, rank, world, local, cpu_sec)
+        if args.frame_len == 1500 and not args.no_9000 and not args.stride and not args.payloadsz:
+            r9 = measure(args, 9000, torch, dist, dev, rank, world, local, cpu_sec / 2)
+            extra = {"by_frame_len": {"1500": {"value": r["value"], "frame_GB_s": r["frame_GB_s"],
+                                               "ms_per_step": r["ms_per_step"]},
+                                      "9000": r9}}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": r["value"],
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": r["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded splitmix64 TRISTAN-over-UDP frames, SURVEY §8(d))",
+        }
+        line.update({k: v for k, v in r.items() if k not in ("value", "ms_per_step")})
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

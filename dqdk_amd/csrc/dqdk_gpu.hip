@@ -83,6 +83,7 @@ struct dqdk_gpu_queue {
     int cu_count = 256;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    hipEvent_t switch_ev = nullptr;  // orders a stream switch after the old stream's work
     uint32_t* d_hist = nullptr;    // table base plane (u32/bin); value = d_hist + d_lo
     uint8_t* d_lo = nullptr;       // table low-byte plane (partitioned sweep)
     uint32_t* d_snap = nullptr;    // u32 snapshot for histogram_device_ptr (lazy)
@@ -110,6 +111,9 @@ struct dqdk_gpu_queue {
     uint64_t raw_cap = 0;
     uint8_t* h_raw = nullptr;       // pinned
     uint64_t h_raw_cap = 0;
+    // async consumer: per-burst first element / length / output offset
+    uint32_t* d_async = nullptr;
+    size_t async_cap = 0;  // bursts
     std::vector<Reg> regs;
     // stage timing
     int timing = 0;
@@ -222,6 +226,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ra.flags = q->cfg.flags;
     ra.port_start = q->cfg.port_start;
     ra.port_end = q->cfg.port_end;
+    ra.histo = q->histo;
     ra.batch_scratch = q->d_batch;
     const bool partitioned = q->histo && q->E && use_partitioned(q, n);
     uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * kHistScratchWords;
@@ -441,6 +446,10 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     *out = nullptr;
     if (cfg->mode > DQDK_MODE_ENERGYHISTO || cfg->payloadsz > (16u << 20))
         return fail_errno(-EINVAL, "queue_create: bad mode or payloadsz");
+    // E <= 65535: a UDP datagram carries at most 65507 B, and the per-frame
+    // out-of-bounds count (u16 in dqdk_gpu_rx_result_t) can then never clamp
+    if (events_per_payload(cfg->mode, cfg->payloadsz) > 0xffffu)
+        return fail_errno(-EINVAL, "queue_create: payloadsz / 16 must be <= 65535 events");
     if ((uint64_t)max_batch * events_per_payload(cfg->mode, cfg->payloadsz) >= (1ull << 31))
         return fail_errno(-EINVAL, "queue_create: max_batch * events per frame must be < 2^31");
     int ndev = dqdk_gpu_device_count();
@@ -503,8 +512,10 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                             ? 1u
                             : (uint32_t)std::max<size_t>(
                                   1, std::min<size_t>(kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1)));
-            q->part2_stride = nk + kStagePad;
-            q->runs_stride = items * kItemOffs;
+            // slots start 16-B aligned (part2's 16-B stores and the slice gather's
+            // dword loads assume it): strides rounded to 8 u16 elements
+            q->part2_stride = (nk + kStagePad + 7) & ~(size_t)7;
+            q->runs_stride = (items * kItemOffs + 7) & ~(size_t)7;
             if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
                 (e = hipMalloc(&q->d_part1, (nk + kStagePad) * 4)) != hipSuccess ||
                 (e = hipMalloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
@@ -548,6 +559,9 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_raw);
     if (q->h_raw)
         (void)hipHostFree(q->h_raw);
+    if (q->switch_ev)
+        (void)hipEventDestroy(q->switch_ev);
+    (void)hipFree(q->d_async);
     if (q->own_stream)
         (void)hipStreamDestroy(q->own_stream);
     delete q;
@@ -558,7 +572,17 @@ int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* s)
 {
     if (!q)
         return -EINVAL;
-    q->stream = (hipStream_t)s;  // verbatim: NULL is the legacy default stream
+    hipStream_t ns = (hipStream_t)s;  // verbatim: NULL is the legacy default stream
+    if (ns == q->stream)
+        return 0;
+    // work already enqueued on the old stream (a batch, staged slice passes)
+    // is ordered before anything enqueued on the new one
+    HIPCHK(hipSetDevice(q->device));
+    if (!q->switch_ev)
+        HIPCHK(hipEventCreateWithFlags(&q->switch_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(q->switch_ev, q->stream));
+    HIPCHK(hipStreamWaitEvent(ns, q->switch_ev, 0));
+    q->stream = ns;
     return 0;
 }
 
@@ -804,6 +828,64 @@ int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint
     if (!rc && total)
         rc = raw_total(q, n, total);
     return rc;
+}
+
+int dqdk_gpu_async_process_device(dqdk_gpu_queue_t* q, const uint8_t* d_ring, uint64_t nelem, const uint32_t* bursts,
+                                  uint32_t nbursts, int strip_wfm, uint8_t* d_out, uint64_t out_cap, uint64_t* total)
+{
+    if (!q || (!d_ring && nelem) || (!bursts && nbursts) || (!d_out && out_cap))
+        return fail_errno(-EINVAL, "async_process_device: null argument");
+    const uint32_t P = q->cfg.payloadsz;
+    // cne_ring elements are multiples of 4 B (src/ds/cne_ring.c:41): the
+    // reference cannot create its ring otherwise
+    if (P == 0 || (P & 3))
+        return fail_errno(-EINVAL, "async_process_device: payloadsz must be a non-zero multiple of 4");
+    const uint32_t len = strip_wfm ? 16u : P;  // src/tristan.c:343
+    std::vector<uint32_t> b((size_t)nbursts * 4);
+    uint64_t e0 = 0, off = 0;
+    for (uint32_t k = 0; k < nbursts; k++) {
+        if (e0 + bursts[k] > nelem || e0 + bursts[k] > 0xffffffffull)
+            return fail_errno(-EINVAL, "async_process_device: bursts overrun the ring");
+        b[4 * k] = (uint32_t)e0;
+        b[4 * k + 1] = bursts[k];
+        b[4 * k + 2] = (uint32_t)off;
+        b[4 * k + 3] = (uint32_t)(off >> 32);
+        off += (uint32_t)(len * bursts[k]);
+        e0 += bursts[k];
+    }
+    if (total)
+        *total = off;
+    if (nbursts == 0)
+        return 0;
+    HIPCHK(hipSetDevice(q->device));
+    if (q->async_cap < nbursts) {
+        HIPCHK(hipStreamSynchronize(q->stream));
+        (void)hipFree(q->d_async);
+        q->d_async = nullptr;
+        q->async_cap = 0;
+        HIPCHK(hipMalloc(&q->d_async, (size_t)nbursts * 4 * sizeof(uint32_t)));
+        q->async_cap = nbursts;
+    }
+    HIPCHK(hipMemcpyAsync(q->d_async, b.data(), b.size() * sizeof(uint32_t), hipMemcpyHostToDevice, q->stream));
+    AsyncArgs aa{};
+    aa.ring = d_ring;
+    aa.payloadsz = P;
+    aa.E = q->E;
+    aa.len = len;
+    aa.nbursts = nbursts;
+    aa.burst = q->d_async;
+    aa.histo = q->histo && q->E;
+    aa.hist = q->d_hist;
+    aa.out = d_out;
+    aa.out_cap = out_cap;
+    aa.cum = (unsigned long long*)q->d_cum;
+    hipLaunchKernelGGL(async_histo_kernel, dim3((nbursts + 3) / 4), dim3(256), 0, q->stream, aa);
+    if (d_out)
+        hipLaunchKernelGGL(async_raw_kernel, dim3(nbursts), dim3(256), 0, q->stream, aa);
+    HIPCHK(hipGetLastError());
+    // b is host memory the copy reads: complete before returning
+    HIPCHK(hipStreamSynchronize(q->stream));
+    return 0;
 }
 
 int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)

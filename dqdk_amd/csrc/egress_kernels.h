@@ -36,6 +36,26 @@ struct RawArgs {
 __global__ void raw_len_kernel(RawArgs a);
 __global__ void raw_copy_kernel(RawArgs a);
 
+// Async consumer (async_processor, src/tristan.c:332-375): burst k of the
+// ring = elements [first[k], first[k] + ret[k]); tristan_process(buffer,
+// len, ret) histograms the burst's FIRST payload ret times and write()s the
+// burst buffer's first len * ret bytes.
+struct AsyncArgs {
+    const uint8_t* ring;   // nelem elements of payloadsz bytes (payloadsz % 4 == 0)
+    uint32_t payloadsz;
+    uint32_t E;            // events per payload (get_energy_events_count)
+    uint32_t len;          // strip_wfm ? 16 : payloadsz (src/tristan.c:343)
+    uint32_t nbursts;
+    const uint32_t* burst; // [4 * nbursts]: first element, ret, output byte offset (lo, hi)
+    int histo;
+    uint32_t* hist;        // the table's u32 base plane
+    uint8_t* out;          // raw stream (nullable)
+    uint64_t out_cap;
+    unsigned long long* cum;  // dqdk_gpu_counters_t words (total_events, total_bytes, oob_events)
+};
+__global__ void async_histo_kernel(AsyncArgs a);
+__global__ void async_raw_kernel(AsyncArgs a);
+
 __global__ void hist_add_kernel(uint32_t* dst, const uint32_t* src, uint64_t n16);
 __global__ void hist_nonzero_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t n16, unsigned long long* count);
 __global__ void hist_combine_kernel(const uint32_t* hist, const uint8_t* lo, uint64_t i0, uint64_t i1, uint32_t* out);

@@ -237,8 +237,6 @@ __global__ __launch_bounds__(kRawThreads) void raw_copy_kernel(RawArgs a)
     s_len[threadIdx.x] = (uint32_t)b;
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.umem, (short)0, (int)(a.umem_size > 0x7fffffffull ? 0x7fffffffull : a.umem_size), 0x00020000);
     for (int f = w; f < kRawThreads; f += kRawThreads / 64) {
         const uint64_t D = s_off[f], S = s_src[f];
         uint64_t len = s_len[f];
@@ -248,6 +246,20 @@ __global__ __launch_bounds__(kRawThreads) void raw_copy_kernel(RawArgs a)
             len = a.out_cap - D;
         if (!len)
             continue;
+        // a buffer resource per frame, based 16 B below the payload (the first
+        // word may start up to 3 B before it) and ending at the UMEM end: every
+        // offset stays far below num_records wherever the payload sits in the
+        // UMEM (payloads past 2 GiB included); a payload longer than that
+        // (u32-wrapped datalen in a > 2 GiB UMEM) takes plain loads
+        // (readfirstlane: f is wave-uniform, so the SRD is scalar -- no waterfall loop)
+        const uint64_t rb0 = S >= 16 ? (S - 16) & ~15ull : 0ull;
+        const uint64_t rb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb0) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb0 >> 32)) << 32);
+        const uint64_t room = a.umem_size - rb;
+        const bool use_rs = len + 32 <= 0x7fffffffull;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.umem + rb), (short)0,
+            __builtin_amdgcn_readfirstlane((int)(room > 0x7fffffffull ? 0x7fffffffull : room)), 0x00020000);
         const uint64_t E = D + len;
         const uint64_t k0 = D >> 2, k1 = (E + 3) >> 2;  // output words touched
         for (uint64_t k = k0 + lane; k < k1; k += 64) {
@@ -256,9 +268,9 @@ __global__ __launch_bounds__(kRawThreads) void raw_copy_kernel(RawArgs a)
             const uint64_t sa = (uint64_t)(s & ~3ll);
             const uint32_t sh = (uint32_t)(s & 3);
             uint32_t w0, w1;
-            if (S < 0x7ffffff0ull) {
-                w0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)sa, 0, 0);
-                w1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)sa + 4u, 0, 0);
+            if (use_rs) {
+                w0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(sa - rb), 0, 0);
+                w1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(sa - rb) + 4u, 0, 0);
             } else {
                 w0 = *(const uint32_t*)(a.umem + sa);
                 w1 = sa + 8 <= a.umem_size ? *(const uint32_t*)(a.umem + sa + 4) : 0u;
@@ -274,6 +286,63 @@ __global__ __launch_bounds__(kRawThreads) void raw_copy_kernel(RawArgs a)
             }
         }
     }
+}
+
+// ---- async consumer ------------------------------------------------------------
+// One wave per burst: the histogram loop of tristan_process runs `ret` times
+// over the SAME buffer (src/tristan.c:314-315), i.e. every in-bounds event of
+// the burst's first payload adds ret to its bin; total_events += E once,
+// total_bytes += len * ret (u32 product, :327-328).
+__global__ __launch_bounds__(256) void async_histo_kernel(AsyncArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t k = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (k >= a.nbursts)
+        return;
+    const uint32_t first = a.burst[4 * k], ret = a.burst[4 * k + 1];
+    if (ret == 0)
+        return;
+    uint32_t oob = 0;
+    if (a.histo) {
+        const uint32_t* ev = (const uint32_t*)(a.ring + (uint64_t)first * a.payloadsz);
+        for (uint32_t e = lane; e < a.E; e += 64) {
+            const uint32_t w0 = ev[4 * e], w1 = ev[4 * e + 1], w2 = ev[4 * e + 2];
+            const uint32_t ch = w0 >> 16;                 // bytes 2-3 (struct energy_evt, src/tristan.h:13-25)
+            const uint32_t bin = (w1 >> 8) & 0xffffu;     // energy:24 >> 8 (bytes 5-6)
+            const uint32_t hc = w2 & 7u;                  // hist_class:3 (byte 8)
+            if (ch >= DQDK_TRISTAN_CHANNELS || hc >= DQDK_TRISTAN_HISTS) {  // histogram_event :236-241
+                oob++;
+                continue;
+            }
+            __hip_atomic_fetch_add(&a.hist[(ch * DQDK_TRISTAN_HISTS + hc) * DQDK_TRISTAN_BINS + bin], ret,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            oob += __shfl_xor(oob, o);
+    }
+    if (lane == 0) {
+        atomicAdd(&a.cum[6], (unsigned long long)a.E);                  // total_events
+        atomicAdd(&a.cum[7], (unsigned long long)(uint32_t)(a.len * ret));  // total_bytes
+        if (oob)
+            atomicAdd(&a.cum[8], (unsigned long long)oob * ret);       // one log line per call per event
+    }
+}
+
+// One block per burst: write(rawdata_fd, buffer, len * ret) (src/tristan.c:319)
+// -- the first len * ret bytes of the burst's elements, dword-aligned.
+__global__ __launch_bounds__(256) void async_raw_kernel(AsyncArgs a)
+{
+    const uint32_t k = blockIdx.x;
+    const uint32_t first = a.burst[4 * k], ret = a.burst[4 * k + 1];
+    // output offset: the bytes of bursts 0..k-1 (a multiple of 4)
+    const uint64_t o4 = ((uint64_t)a.burst[4 * k + 2] | ((uint64_t)a.burst[4 * k + 3] << 32)) / 4;
+    const uint64_t n4 = (uint64_t)(a.len * ret) / 4;
+    const uint32_t* src = (const uint32_t*)(a.ring + (uint64_t)first * a.payloadsz);
+    uint32_t* dst = (uint32_t*)a.out;
+    for (uint64_t i = threadIdx.x; i < n4; i += 256)
+        if (4 * (o4 + i) + 4 <= a.out_cap)
+            dst[o4 + i] = src[i];
 }
 
 __global__ __launch_bounds__(256) void hist_add_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t n16)

@@ -82,6 +82,7 @@ struct RxArgs {
     uint32_t E;
     uint32_t flags;
     uint32_t port_start, port_end;
+    int histo;                // the mode keeps a histogram (is_store_histo, src/tristan.c:65-70)
     uint64_t* batch_scratch;  // [0] = first abort idx, [1..12] = per-batch counters
     uint32_t* cnt1;           // partitioned histogram: bucket counts (+ KEY_NONE records for non-OK frames), or null
 };

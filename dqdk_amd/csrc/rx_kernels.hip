@@ -278,7 +278,9 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
         fi.pseudo = (uint64_t)saddr + (uint64_t)daddr + (uint64_t)(uint32_t)((17u + len16) << 8);
         fi.work |= 2;
     }
-    if (datalen != 0 && a.E != 0)
+    // events are decoded only for a consumer: the histogram (histo_fd > 0,
+    // src/tristan.c:312) or a caller record buffer
+    if (datalen != 0 && a.E != 0 && (a.histo || a.keys))
         fi.work |= 1;
     needB = fi.work != 0;
     if (needB) {
@@ -662,7 +664,8 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
             if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
                 r.status = DQDK_RX_INVALID_UDP_CSUM;
         }
-        r.oob_events = (uint16_t)(r.status == DQDK_RX_OK ? min(sum_oob, 0xffffu) : 0u);
+        // histogram_event's rejections: none without a histogram (E <= 65535, so no clamp)
+        r.oob_events = (uint16_t)(r.status == DQDK_RX_OK && a.histo ? sum_oob : 0u);
     }
     if (live) {
         if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {

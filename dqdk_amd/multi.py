@@ -72,13 +72,18 @@ def merge_queue_histogram(q, dst: int = 0, group=None, buf: torch.Tensor | None 
     if buf is None:
         buf = torch.empty(L.HISTO_ENTRIES, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev)
+    prev = L.lib().dqdk_gpu_queue_stream(q.handle)
+    q.sync()  # the queue's batches and staged slice passes are complete before the copy
     q.set_stream(s.cuda_stream)
-    q.histogram_copy(buf.data_ptr())
-    reduce_histogram(buf, dst=dst, group=group)
-    if dist.get_rank(group) == dst:
-        q.reset_histogram()
-        q.histogram_add(buf.data_ptr())
-    torch.cuda.synchronize(dev)
+    try:
+        q.histogram_copy(buf.data_ptr())
+        reduce_histogram(buf, dst=dst, group=group)
+        if dist.get_rank(group) == dst:
+            q.reset_histogram()
+            q.histogram_add(buf.data_ptr())
+        torch.cuda.synchronize(dev)
+    finally:
+        q.set_stream(prev or 0)
     return buf
 
 
@@ -92,7 +97,8 @@ def fini(q, runtime_ns: int, directory: str, histo_path: str | None = None, dst:
     total = reduce_counters(q.counters(), device=dev, group=group)
     rt = torch.tensor([runtime_ns], dtype=torch.int64, device=dev)
     dist.all_reduce(rt, op=dist.ReduceOp.MAX, group=group)
-    has_histo = q.histogram_device_ptr() is not None
+    from .rx import histo_enabled
+    has_histo = histo_enabled(q.cfg.mode, q.cfg.flags)  # is_store_histo (no table materialised)
     if has_histo:
         merge_queue_histogram(q, dst=dst, group=group)
     if dist.get_rank(group) != dst:

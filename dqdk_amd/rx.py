@@ -136,6 +136,18 @@ class RxQueue:
                 "raw_compact_device")
         return int(tot.value) if sync else None
 
+    def async_process_device(self, ring_ptr: int, nelem: int, bursts, strip_wfm: bool = False,
+                             out_ptr: int | None = None, out_cap: int = 0) -> int:
+        """The async consumer's tristan_process(buffer, len, ret) per burst
+        (async_processor, src/tristan.c:332-375) over a device ring of
+        payloadsz-byte elements; returns the raw stream length."""
+        b = np.ascontiguousarray(bursts, dtype=np.uint32)
+        tot = C.c_uint64()
+        L.check(L.lib().dqdk_gpu_async_process_device(self._h, ring_ptr, nelem, b.ctypes.data, len(b), int(strip_wfm),
+                                                      out_ptr or None, out_cap, C.byref(tot)),
+                "async_process_device")
+        return int(tot.value)
+
     def set_raw_fd(self, fd: int) -> None:
         """Append every host batch's raw payload stream to fd (-1 = off)."""
         L.check(L.lib().dqdk_gpu_queue_set_raw_fd(self._h, fd), "set_raw_fd")

@@ -174,6 +174,24 @@ int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint
                                 uint8_t* d_out, uint64_t out_cap, uint64_t* total);
 int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd); /* -1 = off (default) */
 
+/* ---- async consumer (async_processor, src/tristan.c:332-375) --------------- */
+/* The raw/async modes hand each payload to post_async (src/dqdk.c:220-229):
+ * a ring of elements of payloadsz bytes; one consumer thread fetches them in
+ * bursts of `ret` <= 16 elements (dqdk_async_processor_nfetch) and calls
+ * tristan_process(buffer, len, ret) with len = strip_wfm ? 16 : payloadsz
+ * (:343).  d_ring (DEVICE) holds nelem such elements back to back (e.g. the
+ * batch's raw stream when datalen == payloadsz); bursts[nbursts] (HOST) are
+ * the fetch sizes in order.  Reproduces that call exactly, quirks included:
+ * the histogram counts the FIRST payload of each burst ret times
+ * (:314-315), total_events grows by E once per burst, total_bytes by
+ * len * ret (:327-328), oob_events by ret per rejected event, and the raw
+ * stream receives the first len * ret bytes of each burst (:319) -- written
+ * to d_out (DEVICE, nullable; min(total, out_cap) bytes).  *total (nullable)
+ * = the raw stream's full length.  payloadsz must be a multiple of 4 (the
+ * reference ring's element rule, src/ds/cne_ring.c:41).  Synchronous. */
+int dqdk_gpu_async_process_device(dqdk_gpu_queue_t* q, const uint8_t* d_ring, uint64_t nelem, const uint32_t* bursts,
+                                  uint32_t nbursts, int strip_wfm, uint8_t* d_out, uint64_t out_cap, uint64_t* total);
+
 /* ---- counters / histogram egress ----------------------------------------- */
 int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out); /* cumulative */
 int dqdk_gpu_counters_reset(dqdk_gpu_queue_t* q);

@@ -266,6 +266,50 @@ static inline uint32_t evt_key(const uint8_t* e)
     return (ch * OR_CHANNELHISTO_COUNT + hc) * OR_HISTO_BINS + bin;
 }
 
+uint32_t or_event_key(const uint8_t* evt) { return evt_key(evt); }
+
+/* tristan_process (tristan.c:308-330) with burst = ret, as async_processor
+ * calls it (:343-349): the histogram loop runs `burst` times over the SAME
+ * buffer base (:314-315), the raw write is len * burst bytes from the buffer
+ * start (:319), total_bytes += len * burst (u32 product, :327) and
+ * total_events += E once (:328). */
+int or_async_process(const uint8_t* ring, uint64_t nelem, const uint32_t* bursts, uint32_t nbursts,
+                     const or_cfg_t* cfg, int strip_wfm, or_counters_t* c, uint32_t* hist,
+                     uint8_t* raw_out, uint64_t raw_cap, uint64_t* raw_total)
+{
+    const uint32_t E = or_events_per_payload(cfg->mode, cfg->payloadsz);
+    const int histo = histo_enabled(cfg);
+    const uint32_t len = strip_wfm ? 16u : cfg->payloadsz; /* :343 TRISTAN_HISTO_EVT_SZ */
+    uint64_t e0 = 0, out = 0;
+    for (uint32_t k = 0; k < nbursts; k++) {
+        const uint32_t burst = bursts[k];
+        if (e0 + burst > nelem)
+            return -1;
+        const uint8_t* buf = ring + e0 * cfg->payloadsz;
+        if (histo) {
+            uint32_t oob = 0;
+            for (uint32_t e = 0; e < E; e++) {
+                uint32_t key = evt_key(buf + 16 * (size_t)e);
+                if (key == OR_KEY_NONE)
+                    oob++;
+                else if (hist)
+                    hist[key] += burst;
+            }
+            c->oob_events += (uint64_t)oob * burst;
+        }
+        const uint32_t wlen = len * burst; /* u32, as write()'s count is computed */
+        for (uint32_t b = 0; b < wlen; b++, out++)
+            if (raw_out && out < raw_cap)
+                raw_out[out] = buf[b];
+        c->total_bytes += wlen;
+        c->total_events += E;
+        e0 += burst;
+    }
+    if (raw_total)
+        *raw_total = out;
+    return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* src/dqdk.c -- get_udp_payload / process_frame / fetch_xsk                */
 /* ---------------------------------------------------------------------- */
@@ -340,7 +384,7 @@ static uint64_t frame_extent(uint32_t E, uint32_t flags)
 }
 
 static void process_one(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, const or_cfg_t* cfg,
-                        uint32_t E, or_result_t* r, uint32_t* keys_out, scratch_t* sc)
+                        uint32_t E, int histo, or_result_t* r, uint32_t* keys_out, scratch_t* sc)
 {
     uint64_t ext = frame_extent(E, cfg->flags);
     uint8_t* f;
@@ -378,18 +422,23 @@ static void process_one(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, c
     if (copied && (cfg->flags & OR_F_CSUM_WRITEBACK) && d->addr < umem_size)
         memcpy(umem + d->addr, f, umem_size - d->addr);
 
-    if (v.status != OR_RX_OK || !keys_out)
+    if (v.status != OR_RX_OK || (!keys_out && !histo))
         return;
     /* process_events_unrolled16 (tristan.c:247-304) reads E events from the
-     * payload start regardless of datalen (tristan.c:311, :315). */
+     * payload start regardless of datalen (tristan.c:311, :315).  The OOB
+     * count is histogram_event's: 0 when the mode keeps no histogram
+     * (histo_fd < 0, tristan.c:312), whatever the frame's position in an
+     * aborted batch (a per-frame property; the counter sums accounted frames). */
     const uint8_t* ev = f + v.payload_off;
     uint32_t oob = 0;
     for (uint32_t e = 0; e < E; e++) {
         uint32_t k = evt_key(ev + 16 * (size_t)e);
         oob += (k == OR_KEY_NONE);
-        keys_out[e] = k;
+        if (keys_out)
+            keys_out[e] = k;
     }
-    r->oob_events = (uint16_t)(oob > 0xffff ? 0xffff : oob);
+    if (histo)
+        r->oob_events = (uint16_t)(oob > 0xffff ? 0xffff : oob);
 }
 
 /* Accounting for one frame that fetch_xsk actually processed
@@ -457,7 +506,7 @@ int or_rx_batch(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, uint32_t 
     /* one pass in descriptor order, like the loop at dqdk.c:291-298 */
     for (uint32_t i = 0; i < n; i++) {
         or_result_t* r = &res[i];
-        process_one(umem, umem_size, &d[i], cfg, E, r, keys ? keys + (size_t)i * E : NULL, &sc);
+        process_one(umem, umem_size, &d[i], cfg, E, histo, r, keys ? keys + (size_t)i * E : NULL, &sc);
         if (r->status == OR_RX_FILTER_DROP || r->status == OR_RX_FILTER_PASS) {
             c->filtered_frames++; /* never reaches the XSK ring */
             continue;

@@ -10,13 +10,21 @@
  *     family) is PINNED: tests/test_oracle_ref.py compares every function
  *     here with the reference's own src/tcpip/{ipv4,udp,inet_csum}.c compiled verbatim into
  *     oracle/_ref/ (oracle/Makefile), and tests/golden/ holds fixtures made
- *     from that build (tests/golden/gen_golden.py).
- *   - get_udp_payload / process_frame / fetch_xsk glue (src/dqdk.c) and the
- *     TRISTAN decode (src/tristan.c) are PARITY UNPINNED by reference
- *     execution: both files include dqdk.h, which needs libbpf/libxdp headers
- *     absent from this image, so they are unbuildable here.  They are
- *     restated line by line from the source text (citations below) and
- *     composed from the pinned tcpip primitives.
+ *     from that build (tests/golden/gen_golden.py: F1, F2).
+ *   - the TRISTAN decode (histogram_event, process_events_unrolled16,
+ *     tristan_process incl. its burst form, get_energy_events_count, the
+ *     energy_evt / tristan_histo_t layout; src/tristan.{c,h}) is PINNED:
+ *     oracle/ref_tristan.py compiles those functions extracted verbatim into
+ *     oracle/_ref/libref_tristan.so, tests/golden/gen_tristan.py records
+ *     F3 (events, frame cases, async bursts) and F4 (a 1024-frame batch
+ *     under both accountings) from it, and test_golden.py / test_oracle_ref.py
+ *     check this restatement against them.
+ *   - the get_udp_payload / process_frame / fetch_xsk glue (src/dqdk.c:185-322)
+ *     stays a restatement: dqdk.c's only type, dqdk_worker_t, embeds libxdp
+ *     ring structs absent from this image, so its text cannot be compiled
+ *     without stand-ins.  Every verdict it composes is a pinned tcpip call,
+ *     and F4's expected counters are built by the same composition around
+ *     the reference's own calls.
  *
  * All citations are path:line relative to the reference checkout.
  */
@@ -115,6 +123,11 @@ typedef struct {
 
 uint32_t or_events_per_payload(uint32_t mode, uint32_t payloadsz); /* tristan.c:72-85 */
 
+/* histogram_event (tristan.c:233-245) as a key: the flat index
+ * (ch*6 + hc)*65536 + (energy >> 8) it increments, or OR_KEY_NONE when it
+ * rejects the event as out of bounds. */
+uint32_t or_event_key(const uint8_t* evt);
+
 /* dqdk_forwarder predicate (src/bpf/forwarder.bpf.c:38-96): 0 DROP, 1 PASS, 2 REDIRECT */
 int or_prefilter(const uint8_t* frame, uint32_t len, uint16_t start, uint16_t end);
 
@@ -139,6 +152,20 @@ int or_rx_batch(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, uint32_t 
 double or_rx_batch_threads(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, uint32_t n,
                            const or_cfg_t* cfg, or_result_t* res, or_counters_t* cnt,
                            uint32_t* hist, int threads);
+
+/*
+ * The async consumer (async_processor, tristan.c:332-375) over a ring of
+ * nelem elements of payloadsz bytes (post_async's elements, dqdk.c:220-229),
+ * fetched in bursts of bursts[k] elements (the `ret` of each
+ * dqdk_async_processor_nfetch): tristan_process(buffer, len, ret) with
+ * len = strip_wfm ? 16 : payloadsz (:343).  Adds to cnt->total_events /
+ * total_bytes / oob_events, to hist (may be NULL), and appends the bytes
+ * write() would receive to raw_out (up to raw_cap; *raw_total = full length).
+ * Returns -1 if the bursts overrun the ring.
+ */
+int or_async_process(const uint8_t* ring, uint64_t nelem, const uint32_t* bursts, uint32_t nbursts,
+                     const or_cfg_t* cfg, int strip_wfm, or_counters_t* cnt, uint32_t* hist,
+                     uint8_t* raw_out, uint64_t raw_cap, uint64_t* raw_total);
 
 #ifdef __cplusplus
 }

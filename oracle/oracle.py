@@ -79,6 +79,11 @@ def oracle() -> C.CDLL:
         h.or_events_per_payload.argtypes = [_U32, _U32]
         h.or_rx_batch.restype = C.c_int
         h.or_rx_batch.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), _P, C.POINTER(Counters), _P, _P]
+        h.or_event_key.restype = _U32
+        h.or_event_key.argtypes = [_P]
+        h.or_async_process.restype = C.c_int
+        h.or_async_process.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), C.c_int, C.POINTER(Counters), _P, _P, _U64,
+                                       C.POINTER(_U64)]
         h.or_rx_batch_threads.restype = C.c_double
         h.or_rx_batch_threads.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), _P, C.POINTER(Counters), _P,
                                           C.c_int]
@@ -143,6 +148,33 @@ def rx_batch_threads(umem: np.ndarray, desc: np.ndarray, payloadsz: int, mode: i
                                        res.ctypes.data, C.byref(cnt),
                                        hist.ctypes.data if hist is not None else None, threads)
     return sec, cnt.as_dict()
+
+
+def event_keys(events: np.ndarray) -> np.ndarray:
+    """histogram_event's key per 16-B event (KEY_NONE when out of bounds)."""
+    ev = np.ascontiguousarray(events, dtype=np.uint8).reshape(-1, 16)
+    lib = oracle()
+    base = ev.ctypes.data
+    return np.array([lib.or_event_key(base + 16 * i) for i in range(len(ev))], dtype=np.uint32)
+
+
+def async_process(ring: np.ndarray, bursts, payloadsz: int, mode: int, strip_wfm: bool, flags: int = 0,
+                  hist: np.ndarray | None = None):
+    """async_processor's tristan_process(buffer, len, ret) per burst.
+    Returns (counters dict, raw bytes)."""
+    ring = np.ascontiguousarray(ring, dtype=np.uint8)
+    b = np.ascontiguousarray(bursts, dtype=np.uint32)
+    nelem = ring.size // payloadsz if payloadsz else 0
+    cnt = Counters()
+    cfg = Cfg(payloadsz, mode, flags, 0, 0)
+    cap = int(b.astype(np.uint64).sum()) * max(payloadsz, 16)
+    raw = np.zeros(max(cap, 1), np.uint8)
+    tot = C.c_uint64()
+    rc = oracle().or_async_process(ring.ctypes.data, nelem, b.ctypes.data, len(b), C.byref(cfg), int(strip_wfm),
+                                   C.byref(cnt), hist.ctypes.data if hist is not None else None, raw.ctypes.data,
+                                   raw.size, C.byref(tot))
+    assert rc == 0
+    return cnt.as_dict(), raw[:tot.value].tobytes()
 
 
 def sparse_histogram(keys: np.ndarray, res: np.ndarray, E: int, limit: int | None = None):

@@ -1,0 +1,46 @@
+"""bench.py's multi-GPU plumbing on CPU (gloo): `--gpus N` without torchrun
+starts N fresh ranks itself, times with barrier + max over ranks and prints
+one line on rank 0; a rank count that disagrees with --gpus is an error.
+(--cpu-dry-run swaps the GPU work for a rank-dependent sleep.)"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def run(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, env=e, capture_output=True, text=True,
+                          timeout=240)
+
+
+def test_gpus_n_spawns_n_ranks_and_aggregates():
+    p = run(["--gpus", "2", "--steps", "5", "--warmup", "1", "--frames", "1000", "--cpu-dry-run"])
+    assert p.returncode == 0, p.stderr
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 5 and d["scaling"] == "weak"
+    assert [r["rank"] for r in d["per_gpu"]] == [0, 1]
+    # rank 1 sleeps twice as long per step: the job time is the slowest rank's
+    assert d["per_gpu"][1]["Mpkt_s"] < d["per_gpu"][0]["Mpkt_s"]
+    assert abs(d["value"] - 2 * d["per_gpu"][1]["Mpkt_s"]) / d["value"] < 0.35
+
+
+def test_default_is_one_rank():
+    p = run(["--steps", "3", "--frames", "1000", "--cpu-dry-run"])
+    assert p.returncode == 0, p.stderr
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["per_gpu"] is None
+
+
+def test_world_size_mismatch_is_an_error():
+    p = run(["--gpus", "1", "--steps", "2", "--cpu-dry-run"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert p.returncode == 2
+    assert "WORLD_SIZE=2" in p.stderr

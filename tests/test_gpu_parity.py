@@ -303,6 +303,39 @@ def test_full_size_properties(L, stride, payloadsz):
     assert np.array_equal(hist, hist2)
 
 
+def test_configs1_parse_checksum_only_form():
+    """BASELINE configs[1] exactly as bench.py measures it: 256K x 1500 B,
+    IPv4 + UDP checksums, no histogram, NO record buffer (d_keys = NULL), so
+    the decode does no event work; every frame against the oracle."""
+    _need_gpu()
+    n = 1 << 18
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, threads=16)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_NO_HISTO)
+    res, cnt, _, _, _ = run_gpu(umem, desc, cfg, keys=False)
+    ores, ocnt, _ = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, want_keys=False)
+    np.testing.assert_array_equal(res, ores)  # status, datalen, payload_off, oob_events (0: no histogram)
+    assert cnt == ocnt
+    assert ocnt["invalid_udp_pkts"] > 0 and ocnt["invalid_ip_pkts"] > 0 and ocnt["empty_pkts"] > 0
+
+
+def test_configs2_jumbo_full_batch_vs_oracle():
+    """BASELINE configs[2] at its own size: 256K x 9000 B, full path (IPv4 +
+    UDP checksums, decode, histogram), every frame, record and bin against
+    the oracle."""
+    _need_gpu()
+    n = 1 << 18
+    umem, desc = D.synth_umem(n, 9000, 9216, faulty=True, threads=16)
+    cfg = D.RxConfig(payloadsz=8958, flags=D.F_CSUM)
+    res, cnt, keys, hist, _ = run_gpu(umem, desc, cfg, keys=True, histogram=True)
+    table = np.zeros(D.HISTO_ENTRIES, np.uint32)
+    ores, ocnt, okeys = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, hist=table)
+    np.testing.assert_array_equal(res, ores)
+    assert cnt == ocnt
+    ok = ores["status"] == D.RX_OK
+    np.testing.assert_array_equal(keys.reshape(n, -1)[ok], okeys.reshape(n, -1)[ok])
+    assert np.array_equal(hist, table)
+
+
 @pytest.mark.parametrize("hpath,kernels", [
     (D.F_HISTO_ATOMIC, {"rx_decode", "rx_abort", "rx_count", "rx_histo_atomic"}),
     (D.F_HISTO_PARTITIONED | D.F_HISTO_EAGER, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_hist_prep", "rx_part2",
