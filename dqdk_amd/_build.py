@@ -3,7 +3,9 @@
 Outputs (git-ignored, travel to the GPU box with the snapshot):
   dqdk_amd/lib/libdqdk_gpu.so   -- the product: HIP kernels + C ABI (include/dqdk_gpu.h)
   oracle/liboracle.so           -- test-only C restatement (oracle/Makefile)
+  build/fetch_xsk_harness       -- test-only C consumer of include/dqdk_gpu.h (tests/c/)
   oracle/_ref/libref_tcpip.so   -- the reference's src/tcpip, only where /root/reference exists
+  oracle/_ref/libref_tristan.so -- the reference's TRISTAN decode (oracle/ref_tristan.py), same condition
 """
 from __future__ import annotations
 
@@ -62,6 +64,17 @@ def build_gpu_lib(force: bool = False) -> Path:
     return lib
 
 
+def build_c_harness(lib: Path, force: bool = False) -> Path:
+    """tests/c/fetch_xsk_harness.c: a plain C program compiled against
+    include/dqdk_gpu.h and linked with libdqdk_gpu.so (test-only)."""
+    src = ROOT / "tests" / "c" / "fetch_xsk_harness.c"
+    out = BUILD / "fetch_xsk_harness"
+    if force or _stale(out, [src, ROOT / "include" / "dqdk_gpu.h", lib]):
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-I", str(ROOT / "include"), str(src), "-o", str(out),
+              "-L", str(LIBDIR), "-ldqdk_gpu", "-Wl,-rpath,$ORIGIN/../dqdk_amd/lib", "-Wl,-rpath,/opt/rocm/lib"])
+    return out
+
+
 def build_oracle(force: bool = False) -> None:
     args = ["make", "-s", "-C", str(ROOT / "oracle")]
     if force:
@@ -69,10 +82,14 @@ def build_oracle(force: bool = False) -> None:
     _run(args)
     if (REF / "src" / "tcpip" / "ipv4.c").exists():
         _run(args + ["ref", f"REF={REF}"])
+        tri = ROOT / "oracle" / "_ref" / "libref_tristan.so"
+        if force or _stale(tri, [REF / "src" / "tristan.c", REF / "src" / "tristan.h", ROOT / "oracle" / "ref_tristan.py"]):
+            _run([sys.executable, str(ROOT / "oracle" / "ref_tristan.py"), "--ref", str(REF), "--out", str(tri)])
 
 
 def build_all(force: bool = False) -> None:
-    build_gpu_lib(force)
+    lib = build_gpu_lib(force)
+    build_c_harness(lib, force)
     build_oracle(force)
 
 

@@ -96,19 +96,28 @@ class E2EPipeline:
         for sl in self.slots:  # the previous run has drained every slot
             sl["used"] = False
         lat = []
-        pending = []  # (release time, out event) of batches in flight
+        pending = []  # [release time, its results-in-host-memory event], in batch order
+
+        def poll(block=False):
+            # a batch's latency ends when its D2H event completes (polled from the host)
+            while pending and (block or pending[0][1].query()):
+                if block:
+                    pending[0][1].synchronize()
+                lat.append(time.perf_counter() - pending.pop(0)[0])
+                block = False
+
         t0 = time.perf_counter()
         for b in range(nbatches):
             if period:
                 while time.perf_counter() < t0 + b * period:
-                    pass
+                    poll()
             release = time.perf_counter()
             sl = self.slots[b % self.depth]
             img = b % len(self.imgs)
             if sl["used"]:
                 # slot reuse: batch b - depth's results have reached host memory
-                sl["out"].synchronize()
-                lat.append(time.perf_counter() - pending.pop(0))
+                while len(pending) >= self.depth:
+                    poll(block=True)
             with torch.cuda.stream(self.s_h2d):
                 self._h2d(sl, img)
                 sl["copied"].record(self.s_h2d)
@@ -121,12 +130,13 @@ class E2EPipeline:
                 sl["h_res"].copy_(sl["res"], non_blocking=True)
                 if self.records:
                     sl["h_keys"].copy_(sl["keys"], non_blocking=True)
-                sl["out"].record(self.s_d2h)
+                out = torch.cuda.Event()
+                out.record(self.s_d2h)
             sl["used"] = True
-            pending.append(release)
-        for k in range(len(pending)):
-            self.slots[(nbatches - len(pending) + k) % self.depth]["out"].synchronize()
-            lat.append(time.perf_counter() - pending[k])
+            pending.append([release, out])
+            poll()
+        while pending:
+            poll(block=True)
         self.q.flush_histogram()
         torch.cuda.synchronize(self.dev)
         sec = time.perf_counter() - t0

@@ -1,0 +1,85 @@
+"""The C boundary exercised from C: build/fetch_xsk_harness (tests/c/) includes
+include/dqdk_gpu.h, links libdqdk_gpu.so and runs INTEGRATION.md's fetch_xsk
+patch over an mmap'd + mlock'd UMEM (hugetlb when the host has it) with a
+wrapping RX descriptor ring and fill-ring reuse (src/dqdk.c:109-127, :252-322).
+
+  * one batch = F4's 1,024 frames, wrapping the ring end: the worker stats and
+    GPU counters equal the reference's recorded F4 counters and the CSV equals
+    the reference's table (tests/golden/gen_tristan.py);
+  * 31 batches of 100 over the stream repeated three times (batch abort on):
+    equal to the oracle (pinned to F4) applied batch by batch.
+"""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import dqdk_amd as D
+from oracle import oracle as O
+from test_gpu_egress import ref_csv
+from test_gpu_parity import _need_gpu
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+HARNESS = ROOT / "build" / "fetch_xsk_harness"
+GOLD = Path(__file__).resolve().parent / "golden"
+STATS = ["rcvd_frames", "rcvd_pkts", "rcvd_bytes", "invalid_ip_pkts", "invalid_udp_pkts", "failing_batches",
+         "total_events", "total_bytes", "oob_events", "empty_pkts"]
+
+
+def run_harness(tmp_path, umem, desc, batch, ring, start, repeat, psz, mode, flags):
+    _need_gpu()
+    assert HARNESS.exists(), "build/fetch_xsk_harness not built (python -m dqdk_amd._build)"
+    (tmp_path / "umem.bin").write_bytes(np.ascontiguousarray(umem).tobytes())
+    (tmp_path / "desc.bin").write_bytes(np.ascontiguousarray(desc).tobytes())
+    csv = tmp_path / "histo.csv"
+    p = subprocess.run([str(HARNESS), str(tmp_path / "umem.bin"), str(tmp_path / "desc.bin"), str(batch), str(ring),
+                        str(start), str(repeat), str(psz), str(mode), str(flags), str(csv)],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    out = dict(l.split() for l in p.stdout.splitlines() if l.strip())
+    return {k: int(v) for k, v in out.items()}, csv.read_text()
+
+
+@pytest.mark.parametrize("csum", [0, 1])
+@pytest.mark.parametrize("abort", [0, 1])
+def test_single_wrapping_batch_equals_reference_f4(tmp_path, csum, abort):
+    z = np.load(GOLD / "f4_batch.npz")
+    mode, psz = (int(x) for x in z["cfg"])
+    flags = (D.F_CSUM if csum else 0) | (D.F_BATCH_ABORT if abort else 0)
+    got, csv = run_harness(tmp_path, z["umem"], z["desc"], batch=1024, ring=2048, start=1500, repeat=1, psz=psz,
+                           mode=mode, flags=flags)
+    assert got["wrapped_batches"] == 1 and got["batches"] == 1
+    k = f"csum{csum}_abort{abort}_"
+    want = dict(zip((str(n) for n in z["counter_names"]), (int(x) for x in z[k + "counters"])))
+    for name in STATS:
+        want_v = want[name] if not (name == "failing_batches" and not abort) else 0
+        assert got[name] == want_v, (name, got[name], want_v)
+    assert got["fill_submitted"] == (0 if abort else 1024)  # an aborted batch is not submitted (:317-321)
+    assert csv == ref_csv(z[k + "hist_idx"], z[k + "hist_cnt"].astype(np.uint64))
+
+
+def test_many_batches_over_wrapping_ring(tmp_path):
+    z = np.load(GOLD / "f4_batch.npz")
+    mode, psz = (int(x) for x in z["cfg"])
+    flags = D.F_CSUM | D.F_BATCH_ABORT
+    batch, repeat = 100, 3
+    got, csv = run_harness(tmp_path, z["umem"], z["desc"], batch=batch, ring=256, start=200, repeat=repeat, psz=psz,
+                           mode=mode, flags=flags)
+    stream = np.concatenate([z["desc"]] * repeat)
+    table = np.zeros(O.HISTO_ENTRIES, np.uint32)
+    tot = dict.fromkeys(STATS, 0)
+    umem = z["umem"].copy()
+    for b0 in range(0, len(stream), batch):
+        _, c, _ = O.rx_batch(umem, stream[b0:b0 + batch], psz, mode, flags, want_keys=False, hist=table)
+        for k in STATS:
+            tot[k] += c[k]
+    assert got["batches"] == -(-len(stream) // batch) and got["wrapped_batches"] > 0
+    for k in STATS:
+        assert got[k] == tot[k], (k, got[k], tot[k])
+    nz = np.flatnonzero(table)
+    assert got["histo_nonzero"] == len(nz)
+    assert csv == ref_csv(nz.astype(np.uint32), table[nz].astype(np.uint64))
