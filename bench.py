@@ -65,6 +65,8 @@ def parse_args(argv=None):
     p.add_argument("--histo-eager", action="store_true", help="slice pass after every batch (no staging)")
     p.add_argument("--no-records", action="store_true",
                    help="with --no-histo: pass no record buffer (parse + checksum only, configs[1])")
+    p.add_argument("--records", action="store_true",
+                   help="histogram mode: also write frame-order decoded records (the unfused path)")
     p.add_argument("--no-9000", action="store_true", help="default run: skip the by_frame_len 9000 B measurement")
     p.add_argument("--e2e", action="store_true", help="PCIe-inclusive pipeline (configs[4])")
     p.add_argument("--e2e-frames", type=int, default=1 << 16, help="frames per e2e batch")
@@ -150,6 +152,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
     E = cfg.events
     histo = D.histo_enabled(mode, flags)
     keys_written = histo or not args.no_records
+    # histogram mode hands the decode no record buffer (the fused decode buckets
+    # its keys itself) unless --records asks for frame-order records as well
+    pass_records = (args.records or not histo) and not args.no_records
 
     # ---- input: queue `rank` of the synthetic UMEM replay, resident in HBM ----
     d_umem, d_desc, desc, sample = synth_to_device(D, torch, dev, n, L, stride, queue=rank)
@@ -164,7 +169,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
 
     def step():
         q.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
-                         None if args.no_records else d_keys.data_ptr())
+                         d_keys.data_ptr() if pass_records else None)
 
     for _ in range(args.warmup):
         step()
@@ -228,6 +233,14 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
 
     # ---- per-kernel algorithmic bytes per launch ------------
     K = n * E  # decoded records per batch
+    if histo and E and not pass_records:
+        # the frame-order records of this batch, for the statistics below only:
+        # a decode-only queue (outside every timed region)
+        with D.RxQueue(local, D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | D.F_NO_HISTO), n) as qr:
+            qr.set_stream(stream.cuda_stream)
+            qr.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
+                              d_keys.data_ptr())
+            torch.cuda.synchronize(dev)
     items = K // (1 << 14) + 284 + 1  # part2 work items (16K-key chunks of the 284 buckets)
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
@@ -241,7 +254,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
         "rx_abort": 8 * n,
         "rx_count": 8 * n,
         "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
-        "rx_part1": 8 * K,  # keys read + bucket runs written
+        # records path: keys read + bucket runs written; fused path: the overflow list only (~0)
+        "rx_part1": 8 * K if pass_records else 0,
+        "rx_fixup": 0,  # fused path: checksum-failed frames taken back (none in the timed workload)
         "rx_hist_prep": 12 * 288,
         "rx_part2": 6 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
@@ -281,8 +296,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                                                      0, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
         pattern["per_frame"] = round(n * (fbytes + 4 * E) / (ms.value * 1e-3) / 1e9, 1)
 
-    hist_kernels = [k for k in ("rx_histo_atomic", "rx_part1", "rx_hist_prep", "rx_part2", "rx_slice_histo",
-                                "rx_slice_heavy") if k in st]
+    hist_kernels = [k for k in ("rx_histo_atomic", "rx_fixup", "rx_part1", "rx_hist_prep", "rx_part2",
+                                "rx_slice_histo", "rx_slice_heavy") if k in st]
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["ms_per_batch"] for k in hist_kernels)
@@ -332,6 +347,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                    "frames_per_batch": n, "frame_len": "mixed 1500/9000" if mixed else L,
                    "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
                    "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
+                   "decode": "fused (keys bucketed in the decode)" if histo and E and not pass_records and n * E >= (4 << 20)
+                   else "records", 
                    "parallelism": f"queue-per-gpu x{world}"},
         "frame_GB_s": round(frame_gbs, 2),
         "per_gpu": per_rank,

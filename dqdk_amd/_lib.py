@@ -64,9 +64,9 @@ MODE_WAVEFORM, MODE_LISTWAVE, MODE_LISTMODE, MODE_ENERGYHISTO = range(4)
 MODES = {"waveform": MODE_WAVEFORM, "listwave": MODE_LISTWAVE, "listmode": MODE_LISTMODE,
          "energy-histo": MODE_ENERGYHISTO}  # src/tristan.c:13-18
 F_CSUM, F_BATCH_ABORT, F_PREFILTER, F_NO_HISTO, F_CSUM_WRITEBACK = 1, 2, 4, 8, 16
-F_HISTO_ATOMIC, F_HISTO_PARTITIONED, F_HISTO_EAGER = 32, 64, 128
+F_HISTO_ATOMIC, F_HISTO_PARTITIONED, F_HISTO_EAGER, F_HISTO_UNFUSED = 32, 64, 128, 256
 KEY_NONE = 0xFFFFFFFF
-TIMING_STAGES = 9
+TIMING_STAGES = 10
 HISTO_CHANNELS, HISTO_HISTS, HISTO_BINS = 1512, 6, 65536
 HISTO_ENTRIES = HISTO_CHANNELS * HISTO_HISTS * HISTO_BINS
 

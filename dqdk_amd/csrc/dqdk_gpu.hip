@@ -47,9 +47,10 @@ int fail_errno(int err, const char* what)
     } while (0)
 
 constexpr int kStages = DQDK_GPU_TIMING_STAGES;
-enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy };
-const char* const kStageNames[kStages] = {"rx_decode", "rx_abort",     "rx_count", "rx_histo_atomic", "rx_part1",
-                                          "rx_hist_prep", "rx_part2", "rx_slice_histo", "rx_slice_heavy"};
+enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy, kStFixup };
+const char* const kStageNames[kStages] = {"rx_decode",    "rx_abort", "rx_count",       "rx_histo_atomic",
+                                          "rx_part1",     "rx_hist_prep", "rx_part2",   "rx_slice_histo",
+                                          "rx_slice_heavy", "rx_fixup"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
@@ -94,6 +95,12 @@ struct dqdk_gpu_queue {
     uint16_t* d_part2 = nullptr;
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
+    uint32_t* d_fix = nullptr;     // fused path: decoded frames that failed afterwards (max_batch)
+    uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions
+    uint64_t ovf_blk_elems = 0;
+    uint64_t fused_elems = 0;      // fused path: pieces region (0: the fused path is off)
+    uint64_t nk_max = 0;           // max_batch * E
+    uint64_t scratch_words = 0;    // hist_scratch_words(nk_max) per staged slot
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     // Partitioned batches stage their slice-sorted keys (part2 + runs +
     // scratch, one slot each); the slice pass -- which sweeps the low-byte
@@ -192,7 +199,8 @@ int hist_flush(dqdk_gpu_queue* q)
     ha.part2 = q->d_part2;
     ha.runs = q->d_runs;
     ha.nslots = q->hist_pending;
-    ha.scratch_stride = kHistScratchWords;
+    ha.scratch_stride = (uint32_t)q->scratch_words;
+    ha.heavy_off = (uint32_t)heavy_off(q->nk_max);
     ha.part2_stride = q->part2_stride;
     ha.runs_stride = q->runs_stride;
     q->hist_pending = 0;
@@ -206,6 +214,16 @@ int hist_flush(dqdk_gpu_queue* q)
     }
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+// Windows per wave per fused round: the block's 16 waves stage at most
+// 16 * W * min(E, 128) keys per round, ~70 % of the LDS stage on average
+// (kFCap keys per bucket), so a bucket rarely overflows its stage.
+uint32_t fused_round_windows(uint32_t E)
+{
+    const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
+    const uint32_t w = (uint32_t)(0.7 * kFCap * kL1Buckets / (kFWaves * epw));
+    return std::max<uint32_t>(kRingW, std::min<uint32_t>(64, w / kRingW * kRingW));
 }
 
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
@@ -229,17 +247,43 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ra.histo = q->histo;
     ra.batch_scratch = q->d_batch;
     const bool partitioned = q->histo && q->E && use_partitioned(q, n);
-    uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * kHistScratchWords;
-    ra.cnt1 = partitioned ? slot_scratch + kOffCnt1 : nullptr;
+    // Fused decode + bucketing: the batch's keys never exist in frame order.
+    // Not when the caller wants those records, nor under batch-abort
+    // accounting (the frames after the first failure are known only after
+    // the decode; the records path counts exactly the accounted frames).
+    const FusedGeom fg = fused_geom(n, q->E, (uint64_t)q->cu_count);
+    const bool fused = partitioned && !d_keys && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT) && q->d_fix &&
+                       !(q->cfg.flags & DQDK_GPU_F_HISTO_UNFUSED) &&
+                       (uint64_t)kL1Buckets * fg.region <= q->fused_elems;
+    uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * q->scratch_words;
+    ra.cnt1 = partitioned && !fused ? slot_scratch + kOffCnt1 : nullptr;
     if (partitioned)
         HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
-    const uint32_t nblk = (n + kTile - 1) / kTile;
+    if (fused) {
+        ra.keys = nullptr;  // no frame-order records
+        ra.scratch = slot_scratch;
+        ra.part1 = q->d_part1;
+        ra.piece_cap = fg.cap;
+        ra.region = fg.region;
+        ra.ovf = q->d_keys;
+        ra.fix = q->d_fix;
+        ra.round_windows = fused_round_windows(q->E);
+        const uint32_t nsuper = (n + 64 * kFWaves - 1) / (64 * kFWaves);
+        const uint32_t grid = fg.grid;
+        // private overflow regions: every key of a block's super-tiles fits its region
+        ra.ovf_blk = q->d_ovf_blk;
+        ra.ovf_blk_cap = (uint32_t)(((nsuper + grid - 1) / grid) * (uint64_t)(64 * kFWaves) * q->E);
+        if ((uint64_t)ra.ovf_blk_cap * grid > q->ovf_blk_elems)
+            return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
+        StageTimer t(q, kStDecode);
+        hipLaunchKernelGGL(rx_decode_fused_kernel, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+    } else {
+        const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
 #define DQDK_DEC_BLOCKS_PER_CU 16u
 #endif
-    const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * DQDK_DEC_BLOCKS_PER_CU);
-    {
+        const uint32_t grid_dec = std::min<uint32_t>(nblk, (uint32_t)q->cu_count * DQDK_DEC_BLOCKS_PER_CU);
         StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_decode_kernel, dim3(grid_dec), dim3(kTile), 0, q->stream, ra);
     }
@@ -279,23 +323,38 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.part1 = q->d_part1;
         ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
         ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
+        ha.heavy_off = (uint32_t)heavy_off(q->nk_max);
+        if (fused) {
+            ha.keys = q->d_keys;                    // the overflow list
+            ha.total_keys = slot_scratch + kOffOvfN;
+            ha.part1_base = (uint64_t)kL1Buckets * fg.region;
+            ha.fused = 1;
+            ha.fgrid = fg.grid;
+            ha.piece_cap = fg.cap;
+            ha.region = fg.region;
+        }
         if (!partitioned) {
             const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
             StageTimer t(q, kStAtomic);
             hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
         } else {
+            if (fused) {
+                StageTimer t(q, kStFixup);  // piece scans, then (usually) an empty list
+                hipLaunchKernelGGL(rx_fixup_kernel, dim3((kL1Buckets + 3) / 4), dim3(256), 0, q->stream, ra, ha);
+            }
             const uint64_t nkeys = (uint64_t)n * q->E;
             const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
             const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
                                                        (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
-            const uint32_t grid_l2 = std::min<uint32_t>(chunks + kL1Buckets, (uint32_t)q->cu_count * 2u);
+            const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
+                                                        (uint32_t)q->cu_count * 2u);
             {
-                StageTimer t(q, kStPart1);
+                StageTimer t(q, kStPart1);  // fused: groups the overflow list (usually empty)
                 hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ha);
             }
             {
                 StageTimer t(q, kStPrep);
-                hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(64), 0, q->stream, ha);
+                hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(1024), 0, q->stream, ha);
             }
             {
                 StageTimer t(q, kStPart2);
@@ -501,7 +560,6 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
-            const size_t items = nk / kPartChunk + kL1Buckets + 1;
             // Stage up to kHistKMax batches per slice pass, as many as keep a
             // slice of uniformly spread events at half the 65535 events of the
             // packed-u16 form (the low-byte sweep is amortised over them; a
@@ -514,14 +572,33 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                                   1, std::min<size_t>(kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1)));
             // slots start 16-B aligned (part2's 16-B stores and the slice gather's
             // dword loads assume it): strides rounded to 8 u16 elements
-            q->part2_stride = (nk + kStagePad + 7) & ~(size_t)7;
-            q->runs_stride = (items * kItemOffs + 7) & ~(size_t)7;
+            // part1/part2: the fused decode's segments, then rx_part1's region
+            // (records / overflow); slots start 16-B aligned (part2's 16-B
+            // stores and the slice gather's dword loads assume it)
+            q->nk_max = nk;
+            q->scratch_words = hist_scratch_words(nk);
+            // the fused pieces at max_batch bound those of any smaller batch;
+            // gathered items address them in 32-bit byte offsets per bucket
+            const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->cu_count);
+            q->fused_elems = fg.region * 4u < (1ull << 31) && (uint64_t)kL1Buckets * fg.region < (1ull << 32)
+                                 ? (uint64_t)kL1Buckets * fg.region
+                                 : 0u;
+            const size_t pe = (size_t)part_elems(nk, q->fused_elems);
+            q->part2_stride = (pe + 7) & ~(size_t)7;
+            q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
             if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part1, (nk + kStagePad) * 4)) != hipSuccess ||
+                (e = hipMalloc(&q->d_part1, pe * 4)) != hipSuccess ||
                 (e = hipMalloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
                 (e = hipMalloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t))) != hipSuccess ||
-                (e = hipMalloc(&q->d_hscratch, q->hist_k * kHistScratchWords * sizeof(uint32_t))) != hipSuccess)
+                (e = hipMalloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
+            // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
+            const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
+            const uint64_t grid = fg.grid;
+            q->ovf_blk_elems = grid * ((nsuper + grid - 1) / grid) * (64 * kFWaves) * q->E;
+            if ((e = hipMalloc(&q->d_ovf_blk, q->ovf_blk_elems * 4)) != hipSuccess)
+                return cleanup((fail("hipMalloc(overflow regions)", e), -ENOMEM));
         }
     }
     *out = q;
@@ -553,6 +630,8 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_part2);
     (void)hipFree(q->d_runs);
     (void)hipFree(q->d_hscratch);
+    (void)hipFree(q->d_fix);
+    (void)hipFree(q->d_ovf_blk);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     (void)hipFree(q->d_raw_blk);

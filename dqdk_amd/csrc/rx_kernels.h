@@ -35,7 +35,10 @@ namespace dqdk {
 
 constexpr int kTile = 256;          // frames per K1 tile = threads per block
 constexpr int kWaves = kTile / 64;  // waves per block
-constexpr int kUnroll = 4;          // 1-KiB windows in flight per wave in phase B
+#ifndef DQDK_RINGW
+#define DQDK_RINGW 4
+#endif
+constexpr int kRingW = DQDK_RINGW;  // 2-KiB windows in flight per wave in phase B
 
 // Partitioned histogram geometry.  Keys < 1512*6*65536 = 594,542,592 < 2^30.
 constexpr int kL1Shift = 21;                                // 2^21 bins (8 MB of table) per bucket
@@ -61,16 +64,62 @@ constexpr int kP1MinWaves = kP1Threads / 64 * kP1BlocksPerCu / 4;  // waves per 
 constexpr uint32_t kBucketAlign = 8;  // bucket starts in part1/part2 rounded to 8 keys (16-B part2 stores)
 constexpr uint32_t kStagePad = kL1Buckets * kBucketAlign;  // extra part1/part2 entries for that padding
 
-// u32 scratch words used by the partitioned histogram
-constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket (decode; upper bound)  -- zeroed per batch
-constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket (part1 cursors)   -- zeroed per batch
-constexpr int kOffHeavyN = 574;     // slices listed for the u32 slice form                    -- zeroed per batch
-constexpr int kZeroWords = 576;
-constexpr int kOffOff1 = 576;       // [kL1Buckets + 1] bucket starts in part1/part2 (prep)
-constexpr int kOffIstart = 864;     // [kL1Buckets + 1] first part2 item of each bucket (prep)
-constexpr int kOffHeavy = 1152;     // [kSlices] slices with > 65535 events this batch
-constexpr int kHistScratchWords = kOffHeavy + kSlices;
-constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a bucket)
+// u32 scratch words used by the partitioned histogram (one block per staged batch)
+constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket: decode upper bound (records path) or
+                                    //   overflow keys per bucket (fused path)                 -- zeroed per batch
+constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket by rx_part1         -- zeroed per batch
+constexpr int kOffHeavyN = 576;     // slices listed for the u32 slice form                     -- zeroed per batch
+constexpr int kOffOvfN = 577;       // fused path: keys sent to the overflow list               -- zeroed per batch
+constexpr int kOffFixN = 578;       // fused path: decoded frames whose final status is not OK  -- zeroed per batch
+constexpr int kZeroWords = 584;
+constexpr int kMaxFusedGrid = 256;  // fused decode blocks (one per CU)
+constexpr int kOffOff1 = kZeroWords;  // [kL1Buckets + 1] bucket starts of rx_part1's output (prep)
+constexpr int kOffIstart = kOffOff1 + 288;  // [kL1Buckets + 1] first part2 item of each bucket; [284] = items (prep)
+// fused path: keys of each (bucket, block) piece [kL1Buckets][kMaxFusedGrid] (decode),
+// and their exclusive scans per bucket [kL1Buckets][kMaxFusedGrid + 1] (prep)
+constexpr int kOffPieceN = kOffIstart + 288;
+constexpr int kOffPiecePre = kOffPieceN + kL1Buckets * kMaxFusedGrid;
+constexpr int kOffItems = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);  // [2 * items]: (part2 index, keys) (prep)
+constexpr int kSegsPerBucket = 2;  // fused: the bucket's pieces (one gathered sequence), then rx_part1's overflow run
+// items of a batch of nk keys: one per started 16K-key chunk of each segment
+__host__ __device__ constexpr uint64_t max_items(uint64_t nk) { return nk / 16384 + (uint64_t)kL1Buckets * kSegsPerBucket + 1; }
+// words of one slot: the fixed part, the item table, the heavy-slice list
+__host__ __device__ constexpr uint64_t hist_scratch_words(uint64_t nk) { return kOffItems + 2 * max_items(nk) + kSlices; }
+__host__ __device__ constexpr uint64_t heavy_off(uint64_t nk) { return kOffItems + 2 * max_items(nk); }
+constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a segment)
+
+// Fused decode (rx_decode_fused): 1024-thread blocks, one per CU, persistent.
+// Keys of a round are counted into an LDS stage per L1 bucket (kFCap keys
+// each), then appended to the block's piece of that bucket (a private
+// region: no device atomics).  The fused region is [bucket][block][cap]: a
+// bucket's pieces are adjacent, in block order.  Keys past kFCap in a round,
+// or past a full piece, go to the block's overflow region, which rx_part1
+// groups afterwards.
+constexpr int kFWaves = 16;
+constexpr int kFThreads = kFWaves * 64;
+#ifndef DQDK_FCAP
+#define DQDK_FCAP 112
+#endif
+constexpr int kFCap = DQDK_FCAP;
+struct FusedGeom {
+    uint32_t grid;    // decode blocks
+    uint32_t cap;     // keys per piece: 1.25x the block's uniform share + slack, whole 128-B lines
+    uint64_t region;  // keys per bucket: grid pieces + 32 (part2's 16-B store tail)
+};
+__host__ __device__ constexpr FusedGeom fused_geom(uint64_t n, uint64_t E, uint64_t cus)
+{
+    const uint64_t nsuper = (n + kFThreads - 1) / kFThreads;
+    const uint64_t g0 = nsuper < cus ? nsuper : cus;
+    const uint64_t grid = g0 < (uint64_t)kMaxFusedGrid ? (g0 ? g0 : 1) : (uint64_t)kMaxFusedGrid;
+    const uint64_t spt = (nsuper + grid - 1) / grid;
+    const uint64_t cap = ((spt * kFThreads * E * 5 / 4) / kL1Buckets + 64 + 31) & ~31ull;
+    return FusedGeom{(uint32_t)grid, (uint32_t)cap, grid * cap + 32};
+}
+// part1/part2 elements: the fused pieces, then rx_part1's output region
+__host__ __device__ constexpr uint64_t part_elems(uint64_t nk, uint64_t fused_elems)
+{
+    return fused_elems + nk + kStagePad;
+}
 
 struct RxArgs {
     const uint8_t* umem;
@@ -85,6 +134,16 @@ struct RxArgs {
     int histo;                // the mode keeps a histogram (is_store_histo, src/tristan.c:65-70)
     uint64_t* batch_scratch;  // [0] = first abort idx, [1..12] = per-batch counters
     uint32_t* cnt1;           // partitioned histogram: bucket counts (+ KEY_NONE records for non-OK frames), or null
+    // fused path (rx_decode_fused) only:
+    uint32_t* scratch;        // the slot's histogram scratch (piece sizes, overflow / fixup counts)
+    uint32_t* part1;          // pieces [bucket][block] of piece_cap keys
+    uint32_t piece_cap;
+    uint64_t region;          // keys per bucket (fused_geom)
+    uint32_t* ovf;            // overflow list (n*E keys)
+    uint32_t* ovf_blk;        // per-block private overflow regions (gridDim.x * ovf_blk_cap keys)
+    uint32_t ovf_blk_cap;
+    uint32_t* fix;            // decoded frames whose final status is not OK (n)
+    uint32_t round_windows;   // windows per wave per round (multiple of the ring depth)
 };
 
 struct CountArgs {
@@ -108,9 +167,16 @@ struct HistoArgs {
     uint8_t* lo;        // table low-byte plane: the partitioned path's per-batch sweep
                         // (bin value = hist[bin] + lo[bin], mod 2^32)
     uint32_t* scratch;  // kHistScratchWords
-    uint32_t* part1;    // n*E keys grouped by bucket
-    uint16_t* part2;    // n*E slice-local keys (key & 16383), each 16K chunk of a bucket sorted by slice
-    uint16_t* runs;     // [items][kItemOffs] slice run starts inside each chunk
+    uint32_t* part1;    // keys grouped by bucket (rx_part1's region starts at part1_base)
+    uint64_t part1_base;  // first element of rx_part1's output (0, or after the fused pieces)
+    uint16_t* part2;    // slice-local keys (key & 16383) at the same indices, each 16K item sorted by slice
+    uint16_t* runs;     // [items][kItemOffs] slice run starts inside each item
+    const uint32_t* total_keys;  // rx_part1 input length on the device (overflow list), or null: limit * E
+    uint32_t fused;     // the keys are the fused decode's pieces + rx_part1's run of its overflow
+    uint32_t fgrid;     // fused: decode blocks (pieces per bucket)
+    uint32_t piece_cap;
+    uint64_t region;
+    uint32_t heavy_off; // scratch word of the heavy-slice list
     // the slice pass runs over nslots staged batches: batch k's scratch,
     // part2 keys and run offsets sit k strides (elements) after the first
     uint32_t nslots;
@@ -119,6 +185,8 @@ struct HistoArgs {
 };
 
 __global__ void rx_decode_kernel(RxArgs a);
+__global__ void rx_decode_fused_kernel(RxArgs a);
+__global__ void rx_fixup_kernel(RxArgs a, HistoArgs h);
 __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);

@@ -338,10 +338,6 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 // event store to an out-of-range offset), so hipcc counts the ring with
 // vmcnt(N) on every path instead of draining it.
 // ---------------------------------------------------------------------------
-#ifndef DQDK_RINGW
-#define DQDK_RINGW 4
-#endif
-constexpr int kRingW = DQDK_RINGW;
 #ifndef DQDK_LD_AUX
 #define DQDK_LD_AUX 0
 #endif
@@ -517,21 +513,14 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const PFrame& P,
     decode_chunk(v1, P.r, e0 + 64u, Ef, kbase, oob_slot, keys_rsrc, lds.cnt);
 }
 
-__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t wave,
-                                                 DecodeLds& lds)
+// ---- phase A: lane parses frame i and prepares its stream (shared by both decodes) ----
+__device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, FrameInfo& fi,
+                                        dqdk_gpu_rx_result_t& r, LaneFrame& lf, bool& stream)
 {
-    const uint32_t i = tile * 64 + lane;
-    const bool live = i < a.n;
-    const uint32_t wslot0 = wave * 64;
-
-    // ---- phase A: lane parses frame i ----
-    FrameInfo fi;
-    dqdk_gpu_rx_result_t r;
     bool needB = false;
     if (live)
         parse_frame(a, i, fi, r, needB);
-    bool stream = false;
-    LaneFrame lf;
+    stream = false;
     lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
     lf.pk2 = kNoWin | (kNoWin << 16);
     lf.ct = -1;
@@ -560,6 +549,73 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     }
     if (!stream)
         lf.pk1 = 0;
+}
+
+// ---- phase C: lane finishes its own frame (checksum verdict, result) ----
+__device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, bool stream, const FrameInfo& fi,
+                                        dqdk_gpu_rx_result_t& r, uint32_t sum_t, uint32_t sum_oob, const u32x4& tail)
+{
+    if (stream) {
+        if (fi.work & 2) {
+            // tail correction: bytes [keep, 16) of the last checksum chunk lie
+            // past the datagram (the odd-length over-read byte is inside keep)
+            uint32_t corr = 0;
+            if (fi.g.ct >= 0 && fi.g.keep < 16) {
+                const uint32_t tw4[4] = {tail.x, tail.y, tail.z, tail.w};
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const int lo = fi.g.keep - 4 * d;  // bytes of dword d inside the datagram
+                    const uint32_t m = lo <= 0 ? 0xffffffffu : lo >= 4 ? 0u : (0xffffffffu << (8 * lo));
+                    corr = __builtin_amdgcn_udot2(as_u16x2(tw4[d] & m), u16x2{1, 1}, corr, false);
+                }
+            }
+            // udp_csum sums LE words from the UDP start.  tsum summed the words
+            // at even addresses: the same words when the UDP header starts at an
+            // even address; otherwise every word is byte-swapped, and the one's
+            // complement sum of swapped words is the swapped sum (the value
+            // mod 0xffff is all udp_csum_ok depends on; + 0xffff keeps the
+            // check subtraction from wrapping)
+            const uint32_t tsum = sum_t - fi.head - corr;
+            const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
+            uint32_t f = (tsum & 0xffffu) + (tsum >> 16);
+            f = (f & 0xffffu) + (f >> 16);
+            const uint32_t S = even ? tsum : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
+            if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
+                r.status = DQDK_RX_INVALID_UDP_CSUM;
+        }
+        // histogram_event's rejections: none without a histogram (E <= 65535, so no clamp)
+        r.oob_events = (uint16_t)(r.status == DQDK_RX_OK && a.histo ? sum_oob : 0u);
+    }
+    if (live) {
+        if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {
+            r.datalen = 0;
+            r.payload_off = 0;
+        }
+        a.res[i] = r;
+        if ((fi.work & 2) && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {  // udp.c:17 side effect
+            const uint64_t ck = fi.addr + 14 + fi.hs + 6;
+            if (ck + 2 <= a.umem_size) {
+                uint8_t* p = const_cast<uint8_t*>(a.umem) + ck;
+                p[0] = 0;
+                p[1] = 0;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t wave,
+                                                 DecodeLds& lds)
+{
+    const uint32_t i = tile * 64 + lane;
+    const bool live = i < a.n;
+    const uint32_t wslot0 = wave * 64;
+
+    // ---- phase A: lane parses frame i ----
+    FrameInfo fi;
+    dqdk_gpu_rx_result_t r;
+    LaneFrame lf;
+    bool stream;
+    phase_a(a, i, live, fi, r, lf, stream);
 
     // ---- phase B: stream the frames ----
     const uint64_t smask0 = __ballot(stream);
@@ -635,53 +691,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     const uint32_t sum_t = lds.sum[my], sum_oob = lds.cnt[kLdsOob + my];
     lds.sum[my] = 0;
     lds.cnt[kLdsOob + my] = 0;
-    if (stream) {
-        if (fi.work & 2) {
-            // tail correction: bytes [keep, 16) of the last checksum chunk lie
-            // past the datagram (the odd-length over-read byte is inside keep)
-            uint32_t corr = 0;
-            if (fi.g.ct >= 0 && fi.g.keep < 16) {
-                const u32x4 t = lds.tail[my];
-                const uint32_t tw4[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const int lo = fi.g.keep - 4 * d;  // bytes of dword d inside the datagram
-                    const uint32_t m = lo <= 0 ? 0xffffffffu : lo >= 4 ? 0u : (0xffffffffu << (8 * lo));
-                    corr = __builtin_amdgcn_udot2(as_u16x2(tw4[d] & m), u16x2{1, 1}, corr, false);
-                }
-            }
-            // udp_csum sums LE words from the UDP start.  tsum summed the words
-            // at even addresses: the same words when the UDP header starts at an
-            // even address; otherwise every word is byte-swapped, and the one's
-            // complement sum of swapped words is the swapped sum (the value
-            // mod 0xffff is all udp_csum_ok depends on; + 0xffff keeps the
-            // check subtraction from wrapping)
-            const uint32_t tsum = sum_t - fi.head - corr;
-            const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
-            uint32_t f = (tsum & 0xffffu) + (tsum >> 16);
-            f = (f & 0xffffu) + (f >> 16);
-            const uint32_t S = even ? tsum : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
-            if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
-                r.status = DQDK_RX_INVALID_UDP_CSUM;
-        }
-        // histogram_event's rejections: none without a histogram (E <= 65535, so no clamp)
-        r.oob_events = (uint16_t)(r.status == DQDK_RX_OK && a.histo ? sum_oob : 0u);
-    }
-    if (live) {
-        if (r.status != DQDK_RX_OK && r.status != DQDK_RX_EMPTY) {
-            r.datalen = 0;
-            r.payload_off = 0;
-        }
-        a.res[i] = r;
-        if ((fi.work & 2) && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {  // udp.c:17 side effect
-            const uint64_t ck = fi.addr + 14 + fi.hs + 6;
-            if (ck + 2 <= a.umem_size) {
-                uint8_t* p = const_cast<uint8_t*>(a.umem) + ck;
-                p[0] = 0;
-                p[1] = 0;
-            }
-        }
-    }
+    phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
     // the partitioned histogram reads records by index only: every non-OK
     // frame gets KEY_NONE records (rare; after this wave's speculative stores)
     const bool fill = live && a.cnt1 && a.keys && a.E && r.status != DQDK_RX_OK;
@@ -717,6 +727,346 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
         for (int b = tid; b < kL1Buckets; b += kTile)
             if (lds.cnt[b])
                 atomicAdd(&a.cnt1[b], lds.cnt[b]);
+    }
+}
+
+// ===========================================================================
+// Fused decode: rx_decode + rx_part1 in one persistent kernel.  A block of
+// kFWaves waves takes kFWaves 64-frame tiles at a time (a super-tile); its
+// waves stream their frames exactly as rx_decode does, but a decoded key goes
+// to the block's LDS stage of its L1 bucket (a returning LDS atomic gives its
+// slot) instead of to a frame-order record.  Every round_windows windows the
+// block synchronises and every bucket's staged run is appended to the block's
+// piece of that bucket (fused_geom's [bucket][block][cap] region): the
+// piece cursors are private to the block (one per lane of the owning wave,
+// in a VGPR), so no device atomic is on the path.  Keys past kFCap in a round,
+// or past a full piece, go to the block's private overflow region and from
+// there to the overflow list, which rx_part1 groups like frame-order records.
+// Frames decoded but later failing the UDP checksum are listed for rx_fixup.
+// ===========================================================================
+struct FusedLds {
+    uint32_t stage[kL1Buckets * kFCap + 64];  // (+64: the flush reads 128 slots per bucket)
+    uint32_t scnt[kL1Buckets + 4];   // staged keys per bucket this round (returning LDS atomics)
+    uint32_t sum[kFWaves * 64];      // checksum word sums per frame
+    uint32_t oob[kFWaves * 64];      // out-of-bounds events per frame
+    u32x4 tail[kFWaves * 64];        // last checksum chunk per frame
+    uint32_t wtot[kFWaves];          // windows of each wave's tile
+    uint32_t ovf_n;                  // keys in this block's private overflow region
+};
+
+// Block barrier for LDS hand-offs only.  __syncthreads() is a workgroup
+// release + acquire: on gfx950 that is s_waitcnt vmcnt(0) before s_barrier,
+// which would wait for every ring load in flight and every run store of the
+// flush at each round.  The rounds only exchange LDS data, for which
+// lgkmcnt(0) (this wave's LDS operations performed) is enough.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One event per 16-B chunk (as decode_chunk): the key goes to the LDS stage
+// of its bucket; past kFCap staged keys (rare) it goes to the block's private
+// overflow region.  The overflow store is issued by every lane of every
+// window (dropped out of range unless the key overflows) and its slot comes
+// from an LDS counter: the window loop's VMEM pattern stays fixed, so the
+// compiler waits for ring loads with vmcnt(N) instead of draining the ring (a
+// conditional global atomic or store here would force near-full waits).
+__device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef, uint32_t oob_slot,
+                                            FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc)
+{
+    const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
+    const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
+    const uint32_t ch = x & 0xffffu;
+    const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
+    const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
+    const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
+    const bool inb = ch < kChannels && hc < kHists;                  // histogram_event's bounds (tristan.c:236-241)
+    uint32_t ooff = kOOB;
+    if (e < Ef) {
+        if (inb) {
+            const uint32_t b = key >> kL1Shift;
+            const uint32_t slot = atomicAdd(&lds.scnt[b], 1u);
+            if (slot < (uint32_t)kFCap)
+                lds.stage[b * kFCap + slot] = key;
+            else
+                ooff = 4u * atomicAdd(&lds.ovf_n, 1u);
+        } else {
+            atomicAdd(&lds.oob[oob_slot], 1u);
+        }
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, ooff, 0, 0);
+}
+
+// Append the round's staged runs to the block's pieces.  Wave w owns buckets
+// w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece cursor `cur`).
+// All LDS reads of a few buckets are issued before their stores, and every
+// store is issued (its offset dropped past the run): no dependent chain per
+// bucket and a fixed VMEM pattern.  Rare: keys past a full piece go to the
+// block's overflow region (slot from an LDS counter).
+__device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int lane, uint32_t wave, uint32_t& cur,
+                                            __amdgpu_buffer_rsrc_t ovf_rsrc)
+{
+    const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
+    uint32_t c = 0, fit = 0;
+    if (b < (uint32_t)kL1Buckets) {
+        c = min(lds.scnt[b], (uint32_t)kFCap);
+        fit = min(c, a.piece_cap - cur);
+    }
+    const uint32_t base = cur;
+    cur += fit;
+    constexpr int NJ = (kL1Buckets + kFWaves - 1) / kFWaves;
+#ifndef DQDK_FLUSH_G
+#define DQDK_FLUSH_G 6
+#endif
+    constexpr int G = DQDK_FLUSH_G;  // buckets per batch of reads (VGPRs: the load ring stays live)
+    uint32_t* const piece0 = a.part1 + (uint64_t)blockIdx.x * a.piece_cap;
+#pragma unroll 1
+    for (int h = 0; h < (NJ + G - 1) / G; h++) {
+        uint32_t v0[G], v1[G];
+#pragma unroll
+        for (int q = 0; q < G; q++) {
+            const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(h * G + q), (uint32_t)kL1Buckets - 1);
+            v0[q] = lds.stage[bj * kFCap + lane];
+            v1[q] = lds.stage[bj * kFCap + 64 + lane];
+        }
+#pragma unroll
+        for (int q = 0; q < G; q++) {
+            const int j = h * G + q;
+            if (j < NJ) {
+                const uint32_t bj = wave + (uint32_t)kFWaves * (uint32_t)j;
+                const uint32_t fj = rdl(fit, j), bsj = rdl(base, j);
+                const __amdgpu_buffer_rsrc_t prs =
+                    uniform_rsrc(piece0 + (uint64_t)min(bj, (uint32_t)kL1Buckets - 1) * a.region, a.piece_cap * 4u);
+                const uint32_t o = (bsj + (uint32_t)lane) * 4u;
+                __builtin_amdgcn_raw_buffer_store_b32(v0[q], prs, (uint32_t)lane < fj ? o : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(v1[q], prs, (uint32_t)lane + 64u < fj ? o + 256u : kOOB, 0, 0);
+            }
+        }
+    }
+    for (uint64_t m = __ballot(fit < c); m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint32_t bj = wave + (uint32_t)kFWaves * j;
+        const uint32_t fj = rdl(fit, j), nov = rdl(c, j) - fj;
+        uint32_t o = 0;
+        if (lane == 0)
+            o = atomicAdd(&lds.ovf_n, nov);
+        o = rfl(o);
+        for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
+            __builtin_amdgcn_raw_buffer_store_b32(lds.stage[bj * kFCap + fj + t], ovf_rsrc, 4u * (o + t), 0, 0);
+    }
+    if (b < (uint32_t)kL1Buckets)
+        lds.scnt[b] = 0;
+}
+
+__global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
+{
+    __shared__ FusedLds lds;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wave = rfl((uint32_t)(tid >> 6));
+    const uint32_t wslot0 = wave * 64;
+    for (int b = tid; b < kL1Buckets + 4; b += kFThreads)
+        lds.scnt[b] = 0;
+    lds.sum[tid] = 0;
+    lds.oob[tid] = 0;
+    if (tid == 0)
+        lds.ovf_n = 0;
+    __syncthreads();
+    // this block's private overflow region: room for every key of its super-tiles
+    uint32_t* const ovf_blk = a.ovf_blk + (uint64_t)blockIdx.x * a.ovf_blk_cap;
+    const __amdgpu_buffer_rsrc_t ovf_rsrc = uniform_rsrc(ovf_blk, (uint64_t)a.ovf_blk_cap * 4u);
+    if (blockIdx.x == 0 && tid < 17)
+        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
+
+    const uint32_t ntiles = (a.n + 63) / 64;
+    const uint32_t nsuper = (ntiles + kFWaves - 1) / kFWaves;
+    const int W = (int)a.round_windows;
+    uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
+    for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
+        const uint32_t tile = st * kFWaves + wave;
+        const uint32_t i = tile * 64 + (uint32_t)lane;
+        const bool live = tile < ntiles && i < a.n;
+
+        // ---- phase A ----
+        FrameInfo fi;
+        dqdk_gpu_rx_result_t r;
+        LaneFrame lf;
+        bool stream;
+        phase_a(a, i, live, fi, r, lf, stream);
+        const uint64_t smask0 = __ballot(stream);
+        const int total = smask0 ? (int)wave_sum_dpp(pk_nwin(lf.pk1)) : 0;
+        if (lane == 0)
+            lds.wtot[wave] = (uint32_t)total;
+        lds_barrier();
+        int tmax = 0;
+#pragma unroll
+        for (int w = 0; w < kFWaves; w++)
+            tmax = max(tmax, (int)lds.wtot[w]);
+        const int rounds = (tmax + W - 1) / W;  // the same for every wave: the barriers below match
+        lds_barrier();                          // wtot is rewritten by the next super-tile
+
+        // ---- phase B: rounds of W windows, the block's stage flushed after each ----
+        const uint32_t lane16 = (uint32_t)lane * 16u;
+        uint64_t lmask = smask0;
+        uint32_t jl = smask0 ? (uint32_t)__builtin_ctzll(lmask) : 0u;
+        uint32_t wl = 0, lnwin = smask0 ? pk_nwin(rdl(lf.pk1, jl)) : 0u;
+        __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
+        auto issue = [&](u32x4& d0, u32x4& d1) {
+            const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes : kOOB);
+            d0 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo, 0, DQDK_LD_AUX);
+            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u, 0, DQDK_LD_AUX);
+            if (lmask != 0 && ++wl == lnwin) {
+                wl = 0;
+                lmask &= lmask - 1;
+                if (lmask) {
+                    jl = (uint32_t)__builtin_ctzll(lmask);
+                    lnwin = pk_nwin(rdl(lf.pk1, jl));
+                    lrs = frame_rsrc(lf, jl);
+                }
+            }
+        };
+        u32x4 b0[kRingW], b1[kRingW];
+#pragma unroll
+        for (int d = 0; d < kRingW; d++)
+            issue(b0[d], b1[d]);
+        uint64_t pmask = smask0;
+        uint32_t jp = smask0 ? (uint32_t)__builtin_ctzll(pmask) : 0u;
+        uint32_t wp = 0;
+        PFrame P;
+        if (smask0)
+            pframe(a, lf, jp, P);
+        else
+            P = PFrame{0, 0, 0, 0, 0, 0, 0, kNoWin, kNoWin, 0};
+        uint32_t acc0 = 0, acc1 = 0;
+        // one loop over the rounds' windows (the flush inside it, every W
+        // windows): a single back-edge keeps the compiler's vmcnt accounting
+        // of the load ring exact across rounds
+        const int kend = rounds * W;
+        for (int k = 0; k < kend; k += kRingW) {
+#pragma unroll
+            for (int d = 0; d < kRingW; d++) {
+                const bool active = k + d < total;
+                const uint32_t jw = (uint32_t)kWinChunks * wp;
+                if (active && wp >= P.mw) {
+                    const int j0 = (int)jw + lane;
+                    csum_pair(b0[d], b1[d], j0 <= P.ct ? u16x2{1, 1} : u16x2{0, 0},
+                              j0 + 64 <= P.ct ? u16x2{1, 1} : u16x2{0, 0}, acc0, acc1);
+                } else {
+                    csum_pair(b0[d], b1[d], u16x2{1, 1}, u16x2{1, 1}, acc0, acc1);
+                }
+                if (active && wp == P.tw && lane == (int)P.tl)
+                    lds.tail[wslot0 + jp] = P.th ? b1[d] : b0[d];
+                const uint32_t Ef = active ? P.Ef : 0u;
+                const uint32_t e0 = jw + (uint32_t)lane - P.de;
+                fused_chunk(b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
+                fused_chunk(b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
+                if (active && ++wp == P.nwin) {
+                    lds_add_u32((uint32_t)(uintptr_t)&lds.sum[wslot0 + jp], acc0 + acc1);
+                    acc0 = acc1 = 0;
+                    wp = 0;
+                    pmask &= pmask - 1;
+                    if (pmask) {
+                        jp = (uint32_t)__builtin_ctzll(pmask);
+                        pframe(a, lf, jp, P);
+                    }
+                }
+                issue(b0[d], b1[d]);
+            }
+            if ((k + kRingW) % W == 0) {  // end of a round (block-uniform)
+                lds_barrier();
+                fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
+                lds_barrier();
+            }
+        }
+
+        // ---- phase C ----
+        const uint32_t my = wslot0 + (uint32_t)lane;
+        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my];
+        lds.sum[my] = 0;
+        lds.oob[my] = 0;
+        phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
+        // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
+        if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
+            a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
+    }
+    // the keys still staged, then the piece sizes for rx_hist_prep
+    lds_barrier();
+    fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
+    {
+        const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
+        if (b < (uint32_t)kL1Buckets)
+            a.scratch[kOffPieceN + b * kMaxFusedGrid + blockIdx.x] = fcur;
+    }
+    // the block's private overflow region is appended to the overflow list
+    __syncthreads();  // (also orders the region's stores before the copy below)
+    const uint32_t nov = lds.ovf_n;
+    if (nov) {
+        if (tid == 0)
+            lds.scnt[0] = atomicAdd(&a.scratch[kOffOvfN], nov);
+        __syncthreads();
+        const uint32_t o = lds.scnt[0];
+        for (uint32_t t = (uint32_t)tid; t < nov; t += kFThreads) {
+            const uint32_t k = ovf_blk[t];
+            a.ovf[o + t] = k;
+            atomicAdd(&a.scratch[kOffCnt1 + (k >> kL1Shift)], 1u);
+        }
+    }
+}
+
+// Frames the fused decode staged but whose final status is not OK: subtract
+// their events from the table (u32 wrap: +1 then -1 leaves every bin exact).
+// Event bytes are read as the decode read them (zeros at or past umem_size).
+__global__ void __launch_bounds__(256) rx_fixup_kernel(RxArgs a, HistoArgs h)
+{
+    const uint32_t nfix = a.scratch[kOffFixN];
+    const int lane = threadIdx.x & 63;
+    // first, one wave per bucket: the exclusive scan of its piece sizes
+    // (rx_hist_prep's segment sizes, rx_part2's piece starts)
+    for (uint32_t b = (blockIdx.x * 256 + threadIdx.x) >> 6; b < (uint32_t)kL1Buckets; b += (gridDim.x * 256) >> 6) {
+        const uint32_t* cn = a.scratch + kOffPieceN + b * kMaxFusedGrid;
+        uint32_t* pre = a.scratch + kOffPiecePre + b * (kMaxFusedGrid + 1);
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t blk = (uint32_t)lane * 4u + i;
+            v[i] = blk < h.fgrid ? cn[blk] : 0u;
+            sum += v[i];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t x = __shfl_up(incl, o);
+            if (lane >= o)
+                incl += x;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t blk = (uint32_t)lane * 4u + i;
+            if (blk < h.fgrid)
+                pre[blk] = run;
+            run += v[i];
+        }
+        if (lane == 63)
+            pre[h.fgrid] = incl;
+    }
+    for (uint32_t k = (blockIdx.x * 256 + threadIdx.x) >> 6; k < nfix; k += (gridDim.x * 256) >> 6) {
+        const uint32_t i = a.fix[k];
+        const uint64_t addr = a.desc[i].addr;
+        const uint64_t ihl_at = addr + 14;
+        const uint32_t ihl = ihl_at < a.umem_size ? (a.umem[ihl_at] & 0xfu) : 0u;
+        const uint64_t p = addr + 14 + 4 * ihl + 8;  // get_udp_payload's payload (dqdk.c:205-206)
+        for (uint32_t e = (uint32_t)lane; e < a.E; e += 64) {
+            uint8_t ev[10];
+#pragma unroll
+            for (int j = 0; j < 10; j++) {
+                const uint64_t o = p + 16ull * e + (uint64_t)j;
+                ev[j] = o < a.umem_size ? a.umem[o] : (uint8_t)0;
+            }
+            const uint32_t ch = ev[2] | ((uint32_t)ev[3] << 8);
+            const uint32_t hc = ev[8] & 7u;
+            const uint32_t bin = ev[5] | ((uint32_t)ev[6] << 8);
+            if (ch < kChannels && hc < kHists)
+                __hip_atomic_fetch_sub(&h.hist[(ch * kHists + hc) * DQDK_TRISTAN_BINS + bin], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -932,8 +1282,10 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     __shared__ uint32_t loff[kL1Buckets + 1];
     __shared__ uint32_t gdel[kL1Buckets];  // global position - LDS position of each bucket's run
     const int tid = threadIdx.x;
-    const uint32_t limit = frames_limit(a);
-    const uint32_t total = limit * a.E;
+    // records path: the frame-order records of the accounted frames; fused
+    // path: the decode's overflow list (usually empty)
+    const uint32_t total = a.total_keys ? *a.total_keys : frames_limit(a) * a.E;
+    uint32_t* const out = a.part1 + a.part1_base;
     const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
     constexpr int kOwn = (kL1Buckets + kP1Threads - 1) / kP1Threads;  // buckets reserved per thread (1)
@@ -941,7 +1293,7 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     uint32_t key[kP1Keys];
     auto load = [&](uint32_t b0) {
         const uint32_t n0 = min(total - b0, (uint32_t)kP1Chunk);
-        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + b0, (uint64_t)n0 * 4u);
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.keys + b0, (uint64_t)n0 * 4u);  // keys = records or overflow list
 #pragma unroll
         for (int j = 0; j < kP1Keys; j++)
             key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kP1Threads * 4, 0);
@@ -993,39 +1345,93 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
         const uint32_t nkeys = loff[kL1Buckets];
         for (uint32_t p = tid; p < nkeys; p += kP1Threads) {
             const uint32_t k = stage[p];
-            a.part1[p + gdel[k >> kL1Shift]] = k;
+            out[p + gdel[k >> kL1Shift]] = k;
         }
         __syncthreads();
     }
 }
 
-// Bucket starts (scan of the decode's upper bounds) and part2 item starts
-// (scan of ceil(bucket length / chunk)), once per batch.
-__global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
+// Segments -> part2 items, once per batch.  A segment is a sequence of keys
+// of one L1 bucket: records path, rx_part1's run of the bucket (starts = scan
+// of the decode's upper bounds); fused path, the bucket's pieces (one per
+// decode block, adjacent in the fused region, gathered through the scan of
+// their sizes written here) then rx_part1's run of its overflow keys.  Every
+// started 16K-key chunk of a segment is a part2 item; items are numbered
+// bucket by bucket, and the item table holds each item's part2 index (in
+// units of kBucketAlign keys: part1/part2 may pass 2^32 keys) and key count.
+// A gathered item's part2 index is its bucket's region start + its offset in
+// the bucket's key sequence, which is also where rx_part2 finds its pieces.
+__global__ void __launch_bounds__(1024) rx_hist_prep_kernel(HistoArgs a)
 {
-    wave0_excl_scan(a.scratch + kOffCnt1, a.scratch + kOffOff1, kL1Buckets, true, kBucketAlign);
-    const int lane = threadIdx.x;
-    uint32_t v[5], sum = 0;
+    constexpr int kMaxSeg = kL1Buckets * kSegsPerBucket;
+    __shared__ uint32_t off1[kL1Buckets + 1];
+    __shared__ uint32_t ist[kMaxSeg + 1];
+    __shared__ uint32_t ptot[kL1Buckets];
+    __shared__ uint32_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
+    if (a.fused && tid < kL1Buckets)  // (rx_fixup scanned the piece sizes)
+        ptot[tid] = a.scratch[kOffPiecePre + tid * (kMaxFusedGrid + 1) + a.fgrid];
+    __syncthreads();
+    if (tid <= kL1Buckets)
+        a.scratch[kOffOff1 + tid] = (uint32_t)a.part1_base + off1[tid];
+    const int S = a.fused ? kSegsPerBucket : 1;
+    const int nseg = kL1Buckets * S;
+    auto seg = [&](int t, uint32_t& cnt, uint64_t& base) {
+        const int b = t / S, g = t - b * S;
+        if (!a.fused || g == 1) {
+            cnt = a.scratch[kOffCur1 + b];
+            base = a.part1_base + off1[b];
+        } else {
+            cnt = ptot[b];
+            base = (uint64_t)b * a.region;
+        }
+    };
+    // exclusive scan of items per segment: thread t owns segments 3t .. 3t+2
+    uint32_t v[3], sum = 0;
 #pragma unroll
-    for (int j = 0; j < 5; j++) {
-        const int i = lane * 5 + j;
-        v[j] = i < kL1Buckets ? (a.scratch[kOffCur1 + i] + kPartChunk - 1) / kPartChunk : 0u;
+    for (int j = 0; j < 3; j++) {
+        const int t = 3 * tid + j;
+        uint32_t c = 0;
+        uint64_t bs;
+        if (t < nseg)
+            seg(t, c, bs);
+        v[j] = (c + kPartChunk - 1) / kPartChunk;
         sum += v[j];
     }
     uint32_t incl = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
+        const uint32_t x = __shfl_up(incl, o);
         if (lane >= o)
-            incl += t;
+            incl += x;
     }
-    uint32_t run = incl - sum;
+    if (lane == 63)
+        wsum[wave] = incl;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int w = 0; w < wave; w++)
+        woff += wsum[w];
+    uint32_t run = woff + incl - sum;
 #pragma unroll
-    for (int j = 0; j < 5; j++) {
-        const int i = lane * 5 + j;
-        if (i <= kL1Buckets)
-            a.scratch[kOffIstart + i] = run;
+    for (int j = 0; j < 3; j++) {
+        const int t = 3 * tid + j;
+        if (t <= nseg)
+            ist[t] = run;
         run += v[j];
+    }
+    __syncthreads();
+    if (tid <= kL1Buckets)
+        a.scratch[kOffIstart + tid] = ist[tid * S];
+    uint32_t* items = a.scratch + kOffItems;
+    for (int t = tid; t < nseg; t += 1024) {
+        uint32_t c;
+        uint64_t bs;
+        seg(t, c, bs);
+        for (uint32_t j = 0, it = ist[t]; j * (uint32_t)kPartChunk < c; j++, it++) {
+            items[2 * it] = (uint32_t)((bs + (uint64_t)j * kPartChunk) / kBucketAlign);
+            items[2 * it + 1] = min(c - j * (uint32_t)kPartChunk, (uint32_t)kPartChunk);
+        }
     }
 }
 
@@ -1035,42 +1441,90 @@ __global__ void __launch_bounds__(64) rx_hist_prep_kernel(HistoArgs a)
 __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
-    __shared__ uint32_t istart[kL1Buckets + 1];
     __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1];
+    __shared__ uint32_t prow[2][kMaxFusedGrid + 1];
     const int tid = threadIdx.x;
-    for (int b = tid; b <= kL1Buckets; b += kPartThreads)
-        istart[b] = a.scratch[kOffIstart + b];
-    __syncthreads();
-    const uint32_t nitems = istart[kL1Buckets];
+    const uint32_t nitems = a.scratch[kOffIstart + kL1Buckets];
+    const uint32_t* items = a.scratch + kOffItems;
     uint32_t key[kPartKeysPerThread];
-    // item -> its keys [base, base + nk) in part1/part2; loads them into key[]
-    // (out-of-range lanes read 0 and are dropped below)
-    auto geo = [&](uint32_t item, uint32_t& nk, uint32_t& base) {
-        const int b = find_run(istart, kL1Buckets, item);
-        const uint32_t c0 = (item - istart[b]) * (uint32_t)kPartChunk;
-        nk = min(a.scratch[kOffCur1 + b] - c0, (uint32_t)kPartChunk);
-        base = a.scratch[kOffOff1 + b] + c0;
+    // item -> its keys [base, base + nk) in part1/part2 (the prep's item
+    // table); load() puts them in key[] (out-of-range lanes read 0, dropped below)
+    auto geo = [&](uint32_t item, uint32_t& nk, uint64_t& base) {
+        base = (uint64_t)items[2 * item] * kBucketAlign;
+        nk = items[2 * item + 1];
     };
-    auto load = [&](uint32_t base, uint32_t nk) {
-        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
+    // a gathered item (fused path): its bucket's piece starts go to prow[pb]
+    // (then a barrier), and each key's piece is found there
+    auto gathered = [&](uint64_t base) { return a.fused && base < a.part1_base; };
+    auto stage_pieces = [&](uint64_t base, int pb) {
+        if (gathered(base)) {
+            const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
+            if ((uint32_t)tid <= a.fgrid)
+                prow[pb][tid] = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + tid];
+        }
+    };
+    auto load = [&](uint64_t base, uint32_t nk, int pb) {
+        if (gathered(base)) {
+            const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
+            const uint32_t S = (uint32_t)base - b * (uint32_t)a.region;
+            const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)b * a.region, a.region * 4u);
+#ifdef DQDK_DIAG_P2_CONTIG  // timing only: the same keys' region read contiguously (wrong keys)
+            {
+                const __amdgpu_buffer_rsrc_t s2 = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
 #pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)
-            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+                for (int j = 0; j < kPartKeysPerThread; j++)
+                    key[j] = __builtin_amdgcn_raw_buffer_load_b32(s2, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+                return;
+            }
+#endif
+            const uint32_t* pr = prow[pb];
+            uint32_t p = S + (uint32_t)tid, lo = 0, hi = a.fgrid;  // pr[lo] <= p
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pr[mid] <= p)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            // every key's offset first (LDS only), then the 16 loads back to back
+#pragma unroll
+            for (int j = 0; j < kPartKeysPerThread; j++) {
+                p = S + (uint32_t)(j * kPartThreads + tid);
+                while (lo + 1 < a.fgrid && pr[lo + 1] <= p)
+                    lo++;
+                key[j] = p < S + nk ? (lo * a.piece_cap + (p - pr[lo])) * 4u : kOOB;
+            }
+#pragma unroll
+            for (int j = 0; j < kPartKeysPerThread; j++)
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], 0, 0);
+        } else {
+            const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
+#pragma unroll
+            for (int j = 0; j < kPartKeysPerThread; j++)
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+        }
     };
-    uint32_t nk_next = 0, base_next = 0;
+    uint32_t nk_next = 0;
+    uint64_t base_next = 0;
+    int pb = 0;
     if (kP2Pipe && blockIdx.x < nitems) {
         geo(blockIdx.x, nk_next, base_next);
-        load(base_next, nk_next);
+        stage_pieces(base_next, 0);
+        __syncthreads();
+        load(base_next, nk_next, 0);
     }
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-        uint32_t nk = nk_next, base = base_next;
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
+        uint32_t nk = nk_next;
+        uint64_t base = base_next;
         if (!kP2Pipe)
             geo(item, nk, base);
         if (tid < kSubs)
             lcnt[tid] = 0;
+        if (!kP2Pipe)
+            stage_pieces(base, 0);
         __syncthreads();
         if (!kP2Pipe)
-            load(base, nk);
+            load(base, nk, 0);
         // the counting atomic returns each key's rank inside its slice, so the
         // scatter after the scan is a plain LDS store
         uint32_t rank[kPartKeysPerThread / 2];  // two u16 ranks per word (rank < kPartChunk)
@@ -1096,11 +1550,14 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         // the next item's keys load while this one is written out
-        if (kP2Pipe && item + gridDim.x < nitems) {
+        const bool more = kP2Pipe && item + gridDim.x < nitems;
+        if (more) {
             geo(item + gridDim.x, nk_next, base_next);
-            load(base_next, nk_next);
+            stage_pieces(base_next, pb ^ 1);
         }
         __syncthreads();
+        if (more)
+            load(base_next, nk_next, pb ^ 1);
         // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
         // stale LDS past nk lands in the bucket's padding (never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;
@@ -1124,7 +1581,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 // (skewed spectra, hot bins) is appended to a list and redone by the u32
 // form (64 KB LDS) in a second launch over that list.
 struct SliceLds {
-    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads];
+    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads], s_base[kSliceThreads];
     uint32_t total;
 };
 
@@ -1171,6 +1628,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             if (k == 0 && it < i0 + kSliceThreads) {
                 sl.s_lo[tid] = lo;
                 sl.s_hi[tid] = hi;
+                sl.s_base[tid] = sc(k)[kOffItems + 2 * it];  // in kBucketAlign keys
             }
             mine += hi - lo;
         }
@@ -1183,7 +1641,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         return;  // no events for this slice: table untouched
     if (kPacked && total > 0xffffu) {  // a u16 bin could overflow: the u32 form redoes it
         if (tid == 0)
-            a.scratch[kOffHeavy + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
+            a.scratch[a.heavy_off + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
         return;
     }
     const uint64_t sb = (uint64_t)s << kSliceBits;
@@ -1207,7 +1665,6 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     constexpr int kKG = DQDK_SLICE_KG;
     for (uint32_t k = 0; k < a.nslots; k++) {
     const uint32_t i0 = sc(k)[kOffIstart + b], i1 = sc(k)[kOffIstart + b + 1];
-    const uint32_t bstart = sc(k)[kOffOff1 + b];
     const uint16_t* part2 = a.part2 + (uint64_t)k * a.part2_stride;
     for (uint32_t ib = i0; ib < i1; ib += kSliceThreads) {
         const uint32_t nit = min(i1 - ib, (uint32_t)kSliceThreads);
@@ -1217,6 +1674,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 const uint16_t* ro = runs(k) + (uint64_t)(ib + tid) * kItemOffs + sub;
                 sl.s_lo[tid] = ro[0];
                 sl.s_hi[tid] = ro[1];
+                sl.s_base[tid] = sc(k)[kOffItems + 2 * (ib + tid)];
             }
             __syncthreads();
         }
@@ -1231,8 +1689,8 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 khi[q] = jj < nit ? sl.s_hi[jj] : 0u;
                 dlo[q] = klo[q] >> 1;
                 dhi[q] = (khi[q] + 1) >> 1;
-                // item chunks start at multiples of kBucketAlign keys: dword-aligned
-                src[q] = (const uint32_t*)(part2 + bstart + (ib + jj - i0) * (uint32_t)kPartChunk);
+                // items start at multiples of kBucketAlign keys: dword-aligned
+                src[q] = (const uint32_t*)(part2 + (uint64_t)(jj < nit ? sl.s_base[jj] : 0u) * kBucketAlign);
                 steps = max(steps, dhi[q] - dlo[q]);
             }
             for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
@@ -1316,7 +1774,7 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_heavy_kernel(HistoArgs
     __shared__ SliceLds sl;
     const uint32_t n = a.scratch[kOffHeavyN];
     for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-        slice_histo<false>(a, a.scratch[kOffHeavy + k], h, sl);
+        slice_histo<false>(a, a.scratch[a.heavy_off + k], h, sl);
         __syncthreads();
     }
 }

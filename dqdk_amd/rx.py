@@ -219,7 +219,7 @@ class RxQueue:
         """Time only the named stages (None: all)."""
         mask = 0xFFFFFFFF
         if names is not None:
-            all_names = [L.lib().dqdk_gpu_timing_stage_name(k).decode() for k in range(L.TIMING_STAGES)]
+            all_names = [(L.lib().dqdk_gpu_timing_stage_name(k) or b"").decode() for k in range(L.TIMING_STAGES)]
             mask = sum(1 << all_names.index(n) for n in names)
         L.check(L.lib().dqdk_gpu_timing_stages(self._h, mask), "timing_stages")
 

@@ -104,6 +104,10 @@ enum dqdk_gpu_flags {
     DQDK_GPU_F_HISTO_ATOMIC = 1u << 5,      /* one device atomic per event              */
     DQDK_GPU_F_HISTO_PARTITIONED = 1u << 6, /* bucket -> slice -> LDS histogram + RMW   */
     DQDK_GPU_F_HISTO_EAGER = 1u << 7,       /* partitioned: slice pass after every batch */
+    DQDK_GPU_F_HISTO_UNFUSED = 1u << 8,     /* partitioned: decode to frame-order records, then
+                                               bucket them (default: the decode buckets its keys
+                                               itself when no record buffer is passed and the
+                                               accounting is per-packet) */
 };
 
 typedef struct dqdk_gpu_cfg {
@@ -263,11 +267,12 @@ int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame
 /* When enabled, every kernel launch of every batch is bracketed by its own
  * pair of hipEvents on the queue stream; stage k is one kernel, named by
  * dqdk_gpu_timing_stage_name(k):
- *   0 rx_decode  1 rx_abort  2 rx_count  3 rx_histo_atomic
+ *   0 rx_decode (or the fused decode)  1 rx_abort  2 rx_count  3 rx_histo_atomic
  *   4 rx_part1   5 rx_hist_prep  6 rx_part2  7 rx_slice_histo  8 rx_slice_heavy
+ *   9 rx_fixup (fused path: decoded frames whose final status is not OK)
  * timing_read adds up the completed pairs (after syncing the queue stream),
  * writes stage_ms[k] / counts[k] (launches) for k < nstages and clears them. */
-#define DQDK_GPU_TIMING_STAGES 9
+#define DQDK_GPU_TIMING_STAGES 10
 int dqdk_gpu_timing_enable(dqdk_gpu_queue_t* q, int on);
 /* Restrict the bracketing to the stages whose bit is set in stage_mask
  * (default: all); the others launch without events in between. */

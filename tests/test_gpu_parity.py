@@ -55,8 +55,10 @@ def run_gpu(umem, desc, cfg: D.RxConfig, keys=True, histogram=False, q=None):
     return res, cnt, k, hist, umem_after
 
 
-def compare(umem, desc, cfg: D.RxConfig, check_hist=False):
-    gres, gcnt, gkeys, ghist, gumem = run_gpu(umem, desc, cfg, keys=True, histogram=check_hist)
+def compare(umem, desc, cfg: D.RxConfig, check_hist=False, records=True):
+    """records=False passes no record buffer: a partitioned batch then takes
+    the fused decode (keys bucketed in the decode, never in frame order)."""
+    gres, gcnt, gkeys, ghist, gumem = run_gpu(umem, desc, cfg, keys=records, histogram=check_hist)
     oumem = umem.copy()
     ores, ocnt, okeys = O.rx_batch(oumem, desc, cfg.payloadsz, cfg.mode, cfg.flags, cfg.port_start, cfg.port_end)
     np.testing.assert_array_equal(gres["status"], ores["status"])
@@ -65,7 +67,7 @@ def compare(umem, desc, cfg: D.RxConfig, check_hist=False):
     np.testing.assert_array_equal(gres["oob_events"], ores["oob_events"])
     E = cfg.events
     ok = ores["status"] == D.RX_OK
-    if E:
+    if E and records:
         np.testing.assert_array_equal(gkeys.reshape(-1, E)[ok], okeys.reshape(-1, E)[ok])
     for k, v in ocnt.items():
         assert gcnt[k] == v, (k, gcnt[k], v)
@@ -127,6 +129,34 @@ def test_synthetic_parity(L, stride, faulty, payloadsz, mode, flags, hpath):
     cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | hpath)
     ores, ocnt = compare(umem, desc, cfg, check_hist=D.histo_enabled(mode, flags))
     assert (ores["status"] == D.RX_OK).mean() > 0.9
+
+
+FUSED_CASES = [c for c in CASES if c[4] != D.MODE_WAVEFORM and not (c[5] & D.F_NO_HISTO) and c[3] >= 16]
+
+
+@pytest.mark.parametrize("L,stride,faulty,payloadsz,mode,flags", FUSED_CASES)
+def test_fused_decode_parity(L, stride, faulty, payloadsz, mode, flags):
+    """Partitioned batches without a record buffer and per-packet accounting
+    take rx_decode_fused (keys bucketed in LDS, appended to per-XCD segments,
+    checksum-failed frames taken back by rx_fixup); batch-abort falls back to
+    the records path.  Results, counters and the whole table vs the oracle."""
+    umem, desc = D.synth_umem(6000, L, stride, faulty=faulty)
+    cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | D.F_HISTO_PARTITIONED)
+    ores, ocnt = compare(umem, desc, cfg, check_hist=True, records=False)
+    if faulty and flags & D.F_CSUM:
+        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 0  # the fixup has frames to take back
+
+
+@pytest.mark.parametrize("records", [True, False], ids=["records", "fused"])
+def test_fused_decode_hot_bins_overflow(records):
+    """Peaked spectra: one L1 bucket gets most keys, so the fused decode's LDS
+    stage and that bucket's segments overflow into the overflow list, which
+    rx_part1 groups; the table is still exact."""
+    _need_gpu()
+    rng = np.random.default_rng(21)
+    umem, desc = _peaked(20000, 0, rng)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_HISTO_PARTITIONED)
+    compare(umem, desc, cfg, check_hist=True, records=records)
 
 
 @pytest.mark.parametrize("shift", [1, 2, 3, 5, 8, 10, 13, 15])

@@ -118,15 +118,16 @@ def test_f3_events_gpu_equals_reference(f3, hpath):
 
 # ---- F3 (b): frame cases -------------------------------------------------------
 
-@pytest.mark.parametrize("hpath", HPATHS, ids=HIDS)
-def test_f3_frame_cases_gpu_equal_reference(f3, hpath):
+@pytest.mark.parametrize("hpath,records", [(D.F_HISTO_ATOMIC, True), (D.F_HISTO_PARTITIONED, True),
+                                           (D.F_HISTO_PARTITIONED, False)], ids=["atomic", "partitioned", "fused"])
+def test_f3_frame_cases_gpu_equal_reference(f3, hpath, records):
     for i, name in enumerate(str(n) for n in f3["case_names"]):
         p = f"c{i}_"
         mode, psz, E = (int(x) for x in f3[p + "cfg"])
         cfg = D.RxConfig(payloadsz=psz, mode=mode, flags=hpath)
         assert cfg.events == E
         histo = D.histo_enabled(mode, hpath)
-        res, cnt, _, hist, _ = run_gpu(f3[p + "umem"].copy(), f3[p + "desc"], cfg, keys=True, histogram=histo)
+        res, cnt, _, hist, _ = run_gpu(f3[p + "umem"].copy(), f3[p + "desc"], cfg, keys=records, histogram=histo)
         np.testing.assert_array_equal(res["status"], f3[p + "status"], err_msg=name)
         ok = res["status"] == D.RX_OK
         np.testing.assert_array_equal(res["datalen"][ok], f3[p + "datalen"][ok], err_msg=name)
@@ -184,15 +185,16 @@ def test_async_rejects_what_the_reference_ring_cannot_hold():
 
 # ---- F4: one fetch_xsk batch ---------------------------------------------------
 
-@pytest.mark.parametrize("hpath", HPATHS, ids=HIDS)
+@pytest.mark.parametrize("hpath,records", [(D.F_HISTO_ATOMIC, True), (D.F_HISTO_PARTITIONED, True),
+                                           (D.F_HISTO_PARTITIONED, False)], ids=["atomic", "partitioned", "fused"])
 @pytest.mark.parametrize("csum", [0, 1])
 @pytest.mark.parametrize("abort", [0, 1])
-def test_f4_batch_gpu_equals_reference(abort, csum, hpath):
+def test_f4_batch_gpu_equals_reference(abort, csum, hpath, records):
     z = np.load(GOLD / "f4_batch.npz")
     mode, psz = (int(x) for x in z["cfg"])
     flags = (D.F_CSUM if csum else 0) | (D.F_BATCH_ABORT if abort else 0) | hpath
     cfg = D.RxConfig(payloadsz=psz, mode=mode, flags=flags)
-    res, cnt, _, hist, _ = run_gpu(z["umem"].copy(), z["desc"], cfg, keys=True, histogram=True)
+    res, cnt, _, hist, _ = run_gpu(z["umem"].copy(), z["desc"], cfg, keys=records, histogram=True)
     np.testing.assert_array_equal(res["status"], z[f"status_csum{csum}"])
     ok = res["status"] == D.RX_OK
     np.testing.assert_array_equal(res["datalen"][ok], z[f"datalen_csum{csum}"][ok])

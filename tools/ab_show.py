@@ -1,13 +1,14 @@
-"""Print per-kernel times of an A/B run (tools/ab_run.sh)."""
+#!/usr/bin/env python3
+"""Print value + per-kernel ms of an A/B directory (tools/ab_run.sh output)."""
+import glob
 import json
 import sys
-from pathlib import Path
 
-for f in sorted(Path(sys.argv[1]).glob("*.json")):
+for f in sorted(glob.glob(f"gpurun_out/ab_{sys.argv[1]}/*.json")):
     try:
-        d = json.loads(f.read_text())
+        d = json.loads(open(f).read().strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001
-        print(f.name, "ERR", e)
+        print(f, "ERR", e)
         continue
-    ks = {k: v["avg_ms"] for k, v in d["kernels"].items() if v["avg_ms"] > 0.01}
-    print(f"{f.stem:24s} {d['value']:9.2f}", " ".join(f"{k[3:]}={v:.4f}" for k, v in ks.items()))
+    ks = " ".join(f"{k[3:]}={v['ms_per_batch']:.4f}" for k, v in d["kernels"].items() if v["ms_per_batch"] > 0.003)
+    print(f"{f.split('/')[-1][:-5]:14s} {d['value']:8.2f} {ks}")
