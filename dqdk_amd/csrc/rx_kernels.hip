@@ -1438,6 +1438,15 @@ __global__ void __launch_bounds__(1024) rx_hist_prep_kernel(HistoArgs a)
 // Level 2: each item = one 16K-key chunk of one bucket's part1 run, sorted
 // by slice ((key >> 14) & 127) in LDS and written back in place as u16
 // slice-local keys, with the run starts of its 128 slices.
+// part2's barriers hand off LDS data only (its global reads are read-only
+// inputs, its global writes are not read back by the block): lds_barrier()
+// keeps the next item's key loads in flight across them, where
+// __syncthreads() would wait for every load and store (vmcnt(0))
+#ifdef DQDK_P2_SYNCTHREADS
+#define P2_BARRIER __syncthreads
+#else
+#define P2_BARRIER lds_barrier
+#endif
 __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
@@ -1457,51 +1466,75 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     // (then a barrier), and each key's piece is found there
     auto gathered = [&](uint64_t base) { return a.fused && base < a.part1_base; };
     auto stage_pieces = [&](uint64_t base, int pb) {
+#ifdef DQDK_DIAG_P2_NOSTAGE
+        if (0) {
+#else
         if (gathered(base)) {
+#endif
             const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
             if ((uint32_t)tid <= a.fgrid)
                 prow[pb][tid] = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + tid];
         }
     };
+    // key slots: wave w takes the item's keys [1024w, 1024w + 1024), 64 per
+    // load (slot(j) = 1024w + 64j + lane), so a gathered item's wave crosses
+    // a piece boundary about once: the piece lookup is one uniform compare
+    // per load, with a per-lane walk only where a boundary falls inside it
+    const uint32_t lane = (uint32_t)tid & 63u, wq0 = (uint32_t)tid & ~63u;  // wq0 = 1024 * wave / 16
+    auto slot = [&](int j) { return wq0 * 16u + 64u * (uint32_t)j + lane; };
     auto load = [&](uint64_t base, uint32_t nk, int pb) {
         if (gathered(base)) {
             const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
             const uint32_t S = (uint32_t)base - b * (uint32_t)a.region;
             const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)b * a.region, a.region * 4u);
-#ifdef DQDK_DIAG_P2_CONTIG  // timing only: the same keys' region read contiguously (wrong keys)
-            {
-                const __amdgpu_buffer_rsrc_t s2 = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
-#pragma unroll
-                for (int j = 0; j < kPartKeysPerThread; j++)
-                    key[j] = __builtin_amdgcn_raw_buffer_load_b32(s2, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
-                return;
-            }
-#endif
             const uint32_t* pr = prow[pb];
-            uint32_t p = S + (uint32_t)tid, lo = 0, hi = a.fgrid;  // pr[lo] <= p
+            const uint32_t last = a.fgrid - 1;
+            // the piece of the wave's first key (uniform binary search)
+            const uint32_t p0 = S + wq0 * 16u;
+            uint32_t lo = 0, hi = a.fgrid;
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (pr[mid] <= p)
+                if (rfl(pr[mid]) <= p0)
                     lo = mid;
                 else
                     hi = mid;
             }
-            // every key's offset first (LDS only), then the 16 loads back to back
+            uint32_t cur = rfl(pr[lo]), nxt = rfl(pr[lo + 1]);
+            // common case (no piece boundary and no item end inside the load):
+            // the whole offset but lane*4 is uniform and goes to soffset
+            uint32_t soff[kPartKeysPerThread];
+            const uint32_t end = S + nk;
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++) {
-                p = S + (uint32_t)(j * kPartThreads + tid);
-                while (lo + 1 < a.fgrid && pr[lo + 1] <= p)
+                const uint32_t pj = p0 + 64u * (uint32_t)j;  // the wave's first key of this load
+                while (lo < last && nxt <= pj) {             // uniform advance
                     lo++;
-                key[j] = p < S + nk ? (lo * a.piece_cap + (p - pr[lo])) * 4u : kOOB;
+                    cur = nxt;
+                    nxt = rfl(pr[lo + 1]);
+                }
+                if ((lo < last && nxt < pj + 64u) || pj + 64u > end) {  // per-lane walk
+                    const uint32_t pl = pj + lane;
+                    uint32_t k = lo, c = cur, n = nxt;
+                    while (k < last && n <= pl) {
+                        k++;
+                        c = n;
+                        n = pr[k + 1];
+                    }
+                    key[j] = pl < end ? (k * a.piece_cap + (pl - c)) * 4u : kOOB;
+                    soff[j] = 0;
+                } else {
+                    key[j] = lane * 4u;
+                    soff[j] = (lo * a.piece_cap + (pj - cur)) * 4u;
+                }
             }
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], 0, 0);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], soff[j], 0);
         } else {
             const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (uint32_t)tid * 4u, j * kPartThreads * 4, 0);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wq0 * 16u + lane) * 4u, j * 256, 0);
         }
     };
     uint32_t nk_next = 0;
@@ -1510,7 +1543,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     if (kP2Pipe && blockIdx.x < nitems) {
         geo(blockIdx.x, nk_next, base_next);
         stage_pieces(base_next, 0);
-        __syncthreads();
+        P2_BARRIER();
         load(base_next, nk_next, 0);
     }
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
@@ -1522,7 +1555,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             lcnt[tid] = 0;
         if (!kP2Pipe)
             stage_pieces(base, 0);
-        __syncthreads();
+        P2_BARRIER();
         if (!kP2Pipe)
             load(base, nk, 0);
         // the counting atomic returns each key's rank inside its slice, so the
@@ -1533,20 +1566,20 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             // lanes past the chunk are dropped (and their key overwritten: the
             // build without the overwrite ran 0.78 instead of 0.70 ms at 9000 B,
             // with 29% more HBM reads by PMC; same load instructions)
-            const bool v = (uint32_t)(j * kPartThreads + tid) < nk;
+            const bool v = slot(j) < nk;
             if (!v)
                 key[j] = DQDK_KEY_NONE;
             const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
             rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
-        __syncthreads();
+        P2_BARRIER();
         wave0_excl_scan(lcnt, loff, kSubs, false);
-        __syncthreads();
+        P2_BARRIER();
         if (tid <= kSubs)
             a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++)
-            if ((uint32_t)(j * kPartThreads + tid) < nk)
+            if (slot(j) < nk)
                 stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         // the next item's keys load while this one is written out
@@ -1555,7 +1588,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             geo(item + gridDim.x, nk_next, base_next);
             stage_pieces(base_next, pb ^ 1);
         }
-        __syncthreads();
+        P2_BARRIER();
         if (more)
             load(base_next, nk_next, pb ^ 1);
         // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
@@ -1564,7 +1597,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         u32x4_t* dst4 = (u32x4_t*)(a.part2 + base);
         for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
             dst4[p] = st4[p];
-        __syncthreads();
+        P2_BARRIER();
     }
 }
 
