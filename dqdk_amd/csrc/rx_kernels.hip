@@ -1466,11 +1466,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     // (then a barrier), and each key's piece is found there
     auto gathered = [&](uint64_t base) { return a.fused && base < a.part1_base; };
     auto stage_pieces = [&](uint64_t base, int pb) {
-#ifdef DQDK_DIAG_P2_NOSTAGE
-        if (0) {
-#else
         if (gathered(base)) {
-#endif
             const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
             if ((uint32_t)tid <= a.fgrid)
                 prow[pb][tid] = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + tid];
