@@ -256,7 +256,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
         "rx_histo_atomic": 8 * n + 4 * K,  # + K random RMWs (priced in Gupd/s below)
         # records path: keys read + bucket runs written; fused path: the overflow list only (~0)
         "rx_part1": 8 * K if pass_records else 0,
-        "rx_fixup": 0,  # fused path: checksum-failed frames taken back (none in the timed workload)
+        # fused path: the per-bucket scans of the decode's piece sizes (checksum-failed
+        # frames taken back: none in the timed workload)
+        "rx_fixup": 284 * 256 * 4 + 284 * 257 * 4,
         "rx_hist_prep": 12 * 288,
         "rx_part2": 6 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
@@ -311,15 +313,16 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                      "frac_hbm": round(h_bytes / (h_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "random_atomic_Gupd_s": round(atomic_gupd, 2) if atomic_gupd else None}
 
+    fused = st.get("rx_fixup", {}).get("launches", 0) > 0  # rx_fixup runs on the fused path only
     traffic = None
     try:
         pmc = json.loads(Path(args.pmc).read_text())
         w = pmc.get(f"{L}:{'csum' if not args.no_csum else 'nocsum'}:{n}", {})
-        traffic = w.get("rx_decode_kernel", {}).get("hbm_bytes_per_launch")
+        traffic = w.get("rx_decode_fused_kernel" if fused else "rx_decode_kernel", {}).get("hbm_bytes_per_launch")
     except Exception:
         pass
     dec = st.get("rx_decode", {})
-    roofline = {"bound": "hbm", "kernel": "rx_decode",
+    roofline = {"bound": "hbm", "kernel": "rx_decode_fused" if fused else "rx_decode",
                 "achieved": dec.get("GB_s"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dec.get("frac_hbm"), "traffic": traffic,
                 "alg_bytes_per_frame": round(16 + Lm + 8 + (4 * E if keys_written else 0), 1),
@@ -347,8 +350,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                    "frames_per_batch": n, "frame_len": "mixed 1500/9000" if mixed else L,
                    "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
                    "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
-                   "decode": "fused (keys bucketed in the decode)" if histo and E and not pass_records and n * E >= (4 << 20)
-                   else "records", 
+                   "decode": "fused (keys bucketed in the decode)" if fused else "records",
                    "parallelism": f"queue-per-gpu x{world}"},
         "frame_GB_s": round(frame_gbs, 2),
         "per_gpu": per_rank,
