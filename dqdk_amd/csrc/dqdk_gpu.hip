@@ -175,9 +175,10 @@ constexpr uint64_t kPartitionMinKeys = 4u << 20;
 #define DQDK_HIST_KMAX 12
 #endif
 #ifndef DQDK_HIST_SLICE_EVENTS
-#define DQDK_HIST_SLICE_EVENTS 32768
+#define DQDK_HIST_SLICE_EVENTS 49152
 #endif
 constexpr size_t kHistKMax = DQDK_HIST_KMAX;                  // staged batches per slice pass, at most
+static_assert(kHistKMax <= (size_t)kSliceMaxSlots, "the slice pass indexes staged batches in registers");
 constexpr size_t kHistSliceEvents = DQDK_HIST_SLICE_EVENTS;  // staged events per slice, target
 
 bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)

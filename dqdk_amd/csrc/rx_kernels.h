@@ -50,6 +50,7 @@ constexpr int kPartThreads = 1024;                          // part1/part2 block
 constexpr int kPartKeysPerThread = 16;
 constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 16384 keys staged in LDS
 constexpr int kSliceThreads = 512;
+constexpr int kSliceMaxSlots = 16;  // staged batches one slice pass can take
 #ifndef DQDK_P1_KEYS
 #define DQDK_P1_KEYS 32
 #endif

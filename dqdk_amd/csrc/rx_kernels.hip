@@ -1611,6 +1611,8 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 // form (64 KB LDS) in a second launch over that list.
 struct SliceLds {
     uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads], s_base[kSliceThreads];
+    uint8_t s_k[kSliceThreads];
+    uint32_t b_i0[kSliceMaxSlots], b_n[kSliceMaxSlots];  // the bucket's first item / items per staged batch
     uint32_t total;
 };
 
@@ -1622,6 +1624,11 @@ __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
     else
         atomicAdd(&h[k], 1u);
 }
+
+// The runs of one slice over every staged batch form one flat list of
+// (batch, item) entries -- the bucket's items of batch 0, then of batch 1,
+// ...; entries [e0, e0 + n) are staged in LDS by one round of loads
+// (kSliceMaxSlots: rx_kernels.h)
 
 // counters: packed ? u16 pairs (8192 words) : u32 (16384 words)
 template <bool kPacked>
@@ -1635,33 +1642,68 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     // staged batch k: its scratch (bucket starts, item starts), u16 keys, run offsets
     auto sc = [&](uint32_t k) { return a.scratch + (uint64_t)k * a.scratch_stride; };
     auto runs = [&](uint32_t k) { return a.runs + (uint64_t)k * a.runs_stride; };
-    bool any = false;
-    for (uint32_t k = 0; k < a.nslots; k++)
-        any |= sc(k)[kOffIstart + b] != sc(k)[kOffIstart + b + 1];
-    if (!any)
-        return;
+    // the bucket's items per staged batch (LDS: registers would be 32 more)
+    if (tid < kSliceMaxSlots) {
+        uint32_t i0 = 0, n = 0;
+        if ((uint32_t)tid < a.nslots) {
+            i0 = sc(tid)[kOffIstart + b];
+            n = sc(tid)[kOffIstart + b + 1] - i0;
+        }
+        sl.b_i0[tid] = i0;
+        sl.b_n[tid] = n;
+    }
     if (tid == 0)
         sl.total = 0;
     u32x4_t* h4 = (u32x4_t*)h;
     for (int c = tid; c < kWords / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
-    // events of this slice = sum of its run lengths over the staged batches;
-    // batch 0's first 512 items' runs stay in LDS
-    uint32_t mine = 0;
-    for (uint32_t k = 0; k < a.nslots; k++) {
-        const uint32_t i0 = sc(k)[kOffIstart + b], i1 = sc(k)[kOffIstart + b + 1];
-        for (uint32_t it = i0 + (uint32_t)tid; it < i1; it += kSliceThreads) {
+    uint32_t nent = 0;
+#pragma unroll
+    for (int k = 0; k < kSliceMaxSlots; k++)
+        nent += sl.b_n[k];
+    if (nent == 0)
+        return;
+    // entry e (< nent) -> its batch k and item
+    auto locate = [&](uint32_t e, uint32_t& k, uint32_t& it) {
+        uint32_t kk = 0, rest = e;
+#pragma unroll
+        for (int q = 0; q < kSliceMaxSlots; q++) {
+            const uint32_t n = sl.b_n[q];
+            if (kk == (uint32_t)q && rest >= n) {
+                rest -= n;
+                kk++;
+            }
+        }
+        k = kk;
+        it = sl.b_i0[kk] + rest;
+    };
+    // entries [e0, e0 + ne) -> LDS: run bounds, item base, batch
+    auto stage = [&](uint32_t e0, uint32_t ne) -> uint32_t {
+        uint32_t mine = 0;
+        if ((uint32_t)tid < ne) {
+            uint32_t k, it;
+            locate(e0 + (uint32_t)tid, k, it);
             const uint16_t* ro = runs(k) + (uint64_t)it * kItemOffs + sub;
             const uint32_t lo = ro[0], hi = ro[1];
-            if (k == 0 && it < i0 + kSliceThreads) {
-                sl.s_lo[tid] = lo;
-                sl.s_hi[tid] = hi;
-                sl.s_base[tid] = sc(k)[kOffItems + 2 * it];  // in kBucketAlign keys
-            }
-            mine += hi - lo;
+            sl.s_lo[tid] = lo;
+            sl.s_hi[tid] = hi;
+            sl.s_base[tid] = sc(k)[kOffItems + 2 * it];  // in kBucketAlign keys
+            sl.s_k[tid] = (uint8_t)k;
+            mine = hi - lo;
         }
-    }
+        return mine;
+    };
+    // s_lo..s_k are written below only after every thread has read b_n
+    __syncthreads();
+    // events of this slice = sum of its run lengths: from the first staged
+    // chunk of entries when it holds them all (the usual case), else a pass
+    // (later chunks first: each thread overwrites only its own LDS slot, and
+    // chunk 0's entries must be the ones left staged)
+    uint32_t mine = 0;
+    for (uint32_t e0 = (uint32_t)kSliceThreads; e0 < nent; e0 += kSliceThreads)
+        mine += stage(e0, min(nent - e0, (uint32_t)kSliceThreads));
+    mine += stage(0, min(nent, (uint32_t)kSliceThreads));
     if (mine)
         atomicAdd(&sl.total, mine);
     __syncthreads();
@@ -1692,19 +1734,11 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
 #endif
     constexpr int kNI = DQDK_SLICE_NI;
     constexpr int kKG = DQDK_SLICE_KG;
-    for (uint32_t k = 0; k < a.nslots; k++) {
-    const uint32_t i0 = sc(k)[kOffIstart + b], i1 = sc(k)[kOffIstart + b + 1];
-    const uint16_t* part2 = a.part2 + (uint64_t)k * a.part2_stride;
-    for (uint32_t ib = i0; ib < i1; ib += kSliceThreads) {
-        const uint32_t nit = min(i1 - ib, (uint32_t)kSliceThreads);
-        if (k != 0 || ib != i0) {  // later batches; buckets with more than 512 items (skewed data)
+    for (uint32_t e0 = 0; e0 < nent; e0 += kSliceThreads) {
+        const uint32_t nit = min(nent - e0, (uint32_t)kSliceThreads);
+        if (e0 != 0) {  // more than 512 entries (skewed data, many staged batches)
             __syncthreads();
-            if ((uint32_t)tid < nit) {
-                const uint16_t* ro = runs(k) + (uint64_t)(ib + tid) * kItemOffs + sub;
-                sl.s_lo[tid] = ro[0];
-                sl.s_hi[tid] = ro[1];
-                sl.s_base[tid] = sc(k)[kOffItems + 2 * (ib + tid)];
-            }
+            stage(e0, nit);
             __syncthreads();
         }
         for (uint32_t j = (uint32_t)wave; j < nit; j += kNI * kWavesS) {
@@ -1719,7 +1753,8 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 dlo[q] = klo[q] >> 1;
                 dhi[q] = (khi[q] + 1) >> 1;
                 // items start at multiples of kBucketAlign keys: dword-aligned
-                src[q] = (const uint32_t*)(part2 + (uint64_t)(jj < nit ? sl.s_base[jj] : 0u) * kBucketAlign);
+                src[q] = (const uint32_t*)(a.part2 + (uint64_t)(jj < nit ? sl.s_k[jj] : 0u) * a.part2_stride +
+                                           (uint64_t)(jj < nit ? sl.s_base[jj] : 0u) * kBucketAlign);
                 steps = max(steps, dhi[q] - dlo[q]);
             }
             for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
@@ -1744,7 +1779,6 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             }
         }
     }
-    }  // staged batch k
     __syncthreads();
     // low-byte plane: thread t owns bins [16t, 16t + 16) and [16(t + 512), +16)
 #pragma unroll
