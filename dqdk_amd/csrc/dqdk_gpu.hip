@@ -218,12 +218,18 @@ int hist_flush(dqdk_gpu_queue* q)
 }
 
 // Windows per wave per fused round: the block's 16 waves stage at most
-// 16 * W * min(E, 128) keys per round, ~70 % of the LDS stage on average
-// (kFCap keys per bucket), so a bucket rarely overflows its stage.
+// 16 * W * min(E, 128) keys per round into 284 * kFCap slots.  Measured
+// (A/B, one box): ~75 % mean fill at 1500 B (W = 16: a 64-frame tile is
+// 4 rounds; 24 with 110 % fill overflowed more than the round saved) and
+// ~115 % at 9000 B (W = 16, 2.85 vs 2.95 ms at W = 12): with every window
+// full of events, fewer rounds win over the keys that overflow to rx_part1.
 uint32_t fused_round_windows(uint32_t E)
 {
     const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
-    const uint32_t w = (uint32_t)(0.7 * kFCap * kL1Buckets / (kFWaves * epw));
+#ifndef DQDK_FUSED_FILL
+#define DQDK_FUSED_FILL (E >= 128 ? 110 : 80)
+#endif
+    const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     return std::max<uint32_t>(kRingW, std::min<uint32_t>(64, w / kRingW * kRingW));
 }
 

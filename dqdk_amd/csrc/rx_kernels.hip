@@ -778,7 +778,7 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
     const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
     const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
     const bool inb = ch < kChannels && hc < kHists;                  // histogram_event's bounds (tristan.c:236-241)
-    uint32_t ooff = kOOB;
+    bool ov = false;
     if (e < Ef) {
         if (inb) {
             const uint32_t b = key >> kL1Shift;
@@ -786,10 +786,24 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
             if (slot < (uint32_t)kFCap)
                 lds.stage[b * kFCap + slot] = key;
             else
-                ooff = 4u * atomicAdd(&lds.ovf_n, 1u);
+                ov = true;
         } else {
             atomicAdd(&lds.oob[oob_slot], 1u);
         }
+    }
+    // overflow slots: one LDS atomic per wave (lanes ranked by mbcnt), not one
+    // per key on the block's single counter (64 lanes on one address serialise)
+    uint32_t ooff = kOOB;
+    const uint64_t om = __ballot(ov);
+    if (om) {
+        const uint32_t first = (uint32_t)__builtin_ctzll(om);
+        uint32_t base = 0;
+        if ((uint32_t)(threadIdx.x & 63) == first)
+            base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
+        base = rdl(base, first);
+        if (ov)
+            ooff = 4u * (base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
     }
     __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, ooff, 0, 0);
 }
@@ -996,17 +1010,22 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
     // the block's private overflow region is appended to the overflow list
     __syncthreads();  // (also orders the region's stores before the copy below)
+    // (the last flush left every stage count at 0: they count the region's
+    // keys per bucket here, then one device atomic per bucket per block)
     const uint32_t nov = lds.ovf_n;
     if (nov) {
         if (tid == 0)
-            lds.scnt[0] = atomicAdd(&a.scratch[kOffOvfN], nov);
+            lds.wtot[0] = atomicAdd(&a.scratch[kOffOvfN], nov);
         __syncthreads();
-        const uint32_t o = lds.scnt[0];
+        const uint32_t o = lds.wtot[0];
         for (uint32_t t = (uint32_t)tid; t < nov; t += kFThreads) {
             const uint32_t k = ovf_blk[t];
             a.ovf[o + t] = k;
-            atomicAdd(&a.scratch[kOffCnt1 + (k >> kL1Shift)], 1u);
+            atomicAdd(&lds.scnt[k >> kL1Shift], 1u);
         }
+        __syncthreads();
+        if (tid < kL1Buckets && lds.scnt[tid])
+            atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
 }
 
