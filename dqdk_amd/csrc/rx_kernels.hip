@@ -1761,30 +1761,35 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             __syncthreads();
         }
         for (uint32_t j = (uint32_t)wave; j < nit; j += kNI * kWavesS) {
-            uint32_t klo[kNI], khi[kNI], dlo[kNI], dhi[kNI];
-            const uint32_t* src[kNI];
+            // an item's run parameters are wave-uniform: scalar registers, and
+            // a buffer descriptor per item whose extent ends at the run's last
+            // dword (so the loads need no per-lane bound)
+            uint32_t klo[kNI], khi[kNI], dlo[kNI];
+            __amdgpu_buffer_rsrc_t src[kNI];
             uint32_t steps = 0;
 #pragma unroll
             for (int q = 0; q < kNI; q++) {
                 const uint32_t jj = j + q * kWavesS;
-                klo[q] = jj < nit ? sl.s_lo[jj] : 0u;
-                khi[q] = jj < nit ? sl.s_hi[jj] : 0u;
+                const bool v = jj < nit;
+                const uint32_t jc = v ? jj : 0u;
+                klo[q] = v ? rfl(sl.s_lo[jc]) : 0u;
+                khi[q] = v ? rfl(sl.s_hi[jc]) : 0u;
                 dlo[q] = klo[q] >> 1;
-                dhi[q] = (khi[q] + 1) >> 1;
+                const uint32_t dhi = (khi[q] + 1) >> 1;
                 // items start at multiples of kBucketAlign keys: dword-aligned
-                src[q] = (const uint32_t*)(a.part2 + (uint64_t)(jj < nit ? sl.s_k[jj] : 0u) * a.part2_stride +
-                                           (uint64_t)(jj < nit ? sl.s_base[jj] : 0u) * kBucketAlign);
-                steps = max(steps, dhi[q] - dlo[q]);
+                const uint16_t* base = a.part2 + (uint64_t)rfl(sl.s_k[jc]) * a.part2_stride +
+                                       (uint64_t)rfl(sl.s_base[jc]) * kBucketAlign;
+                src[q] = uniform_rsrc(base, (uint64_t)dhi * 4u);
+                steps = max(steps, dhi - dlo[q]);
             }
             for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
                 uint32_t w[kNI][kKG];
 #pragma unroll
                 for (int q = 0; q < kNI; q++)
 #pragma unroll
-                    for (int g = 0; g < kKG; g++) {
-                        const uint32_t d = dlo[q] + p0 + 64 * g + lane;
-                        w[q][g] = d < dhi[q] ? src[q][d] : 0u;
-                    }
+                    for (int g = 0; g < kKG; g++)
+                        w[q][g] = __builtin_amdgcn_raw_buffer_load_b32(src[q], (dlo[q] + p0 + 64 * g + lane) * 4u, 0,
+                                                                        0);
 #pragma unroll
                 for (int q = 0; q < kNI; q++)
 #pragma unroll
