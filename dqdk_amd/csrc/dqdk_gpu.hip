@@ -230,7 +230,8 @@ uint32_t fused_round_windows(uint32_t E)
 #define DQDK_FUSED_FILL (E >= 128 ? 110 : 80)
 #endif
     const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
-    return std::max<uint32_t>(kRingW, std::min<uint32_t>(64, w / kRingW * kRingW));
+    const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth
+    return std::max<uint32_t>(kFRingW, std::min<uint32_t>(64, wr));
 }
 
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,

@@ -39,6 +39,10 @@ constexpr int kWaves = kTile / 64;  // waves per block
 #define DQDK_RINGW 4
 #endif
 constexpr int kRingW = DQDK_RINGW;  // 2-KiB windows in flight per wave in phase B
+#ifndef DQDK_FRINGW
+#define DQDK_FRINGW 4
+#endif
+constexpr int kFRingW = DQDK_FRINGW;  // the same for the fused decode (rounds are multiples of it)
 
 // Partitioned histogram geometry.  Keys < 1512*6*65536 = 594,542,592 < 2^30.
 constexpr int kL1Shift = 21;                                // 2^21 bins (8 MB of table) per bucket

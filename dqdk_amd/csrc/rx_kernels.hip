@@ -936,9 +936,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
             }
         };
-        u32x4 b0[kRingW], b1[kRingW];
+        u32x4 b0[kFRingW], b1[kFRingW];
 #pragma unroll
-        for (int d = 0; d < kRingW; d++)
+        for (int d = 0; d < kFRingW; d++)
             issue(b0[d], b1[d]);
         uint64_t pmask = smask0;
         uint32_t jp = smask0 ? (uint32_t)__builtin_ctzll(pmask) : 0u;
@@ -953,9 +953,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         // windows): a single back-edge keeps the compiler's vmcnt accounting
         // of the load ring exact across rounds
         const int kend = rounds * W;
-        for (int k = 0; k < kend; k += kRingW) {
+        for (int k = 0; k < kend; k += kFRingW) {
 #pragma unroll
-            for (int d = 0; d < kRingW; d++) {
+            for (int d = 0; d < kFRingW; d++) {
                 const bool active = k + d < total;
                 const uint32_t jw = (uint32_t)kWinChunks * wp;
                 if (active && wp >= P.mw) {
@@ -983,7 +983,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 issue(b0[d], b1[d]);
             }
-            if ((k + kRingW) % W == 0) {  // end of a round (block-uniform)
+            if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
                 lds_barrier();
                 fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
                 lds_barrier();
