@@ -341,6 +341,9 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 #ifndef DQDK_LD_AUX
 #define DQDK_LD_AUX 0
 #endif
+#ifndef DQDK_FST_AUX  // the fused decode's piece stores
+#define DQDK_FST_AUX 0
+#endif
 #ifndef DQDK_ST_AUX
 #define DQDK_ST_AUX 0
 #endif
@@ -849,8 +852,13 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
                 const __amdgpu_buffer_rsrc_t prs =
                     uniform_rsrc(piece0 + (uint64_t)min(bj, (uint32_t)kL1Buckets - 1) * a.region, a.piece_cap * 4u);
                 const uint32_t o = (bsj + (uint32_t)lane) * 4u;
-                __builtin_amdgcn_raw_buffer_store_b32(v0[q], prs, (uint32_t)lane < fj ? o : kOOB, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(v1[q], prs, (uint32_t)lane + 64u < fj ? o + 256u : kOOB, 0, 0);
+#ifndef DQDK_DIAG_FNOSTORE  // timing diagnostic only: the flush without its stores
+                __builtin_amdgcn_raw_buffer_store_b32(v0[q], prs, (uint32_t)lane < fj ? o : kOOB, 0, DQDK_FST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(v1[q], prs, (uint32_t)lane + 64u < fj ? o + 256u : kOOB, 0,
+                                                      DQDK_FST_AUX);
+#else
+                asm volatile("" ::"v"(v0[q]), "v"(v1[q]), "v"(o), "s"(fj));
+#endif
             }
         }
     }
@@ -869,6 +877,10 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
         lds.scnt[b] = 0;
 }
 
+// kLdAux: the frame loads' cache policy (2 = non-temporal: the frames are
+// read once, and keeping them out of L2 leaves it to the pieces' partial
+// lines; measured faster at 1500 B, slower at 9000 B -- the host picks)
+template <int kLdAux>
 __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 {
     __shared__ FusedLds lds;
@@ -924,8 +936,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
         auto issue = [&](u32x4& d0, u32x4& d1) {
             const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes : kOOB);
-            d0 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo, 0, DQDK_LD_AUX);
-            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u, 0, DQDK_LD_AUX);
+            d0 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo, 0, kLdAux);
+            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u, 0, kLdAux);
             if (lmask != 0 && ++wl == lnwin) {
                 wl = 0;
                 lmask &= lmask - 1;
@@ -983,7 +995,11 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 issue(b0[d], b1[d]);
             }
+#ifdef DQDK_DIAG_FNOFLUSH  // timing diagnostic only: no flush inside the rounds (keys lost)
+            if (false) {
+#else
             if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
+#endif
                 lds_barrier();
                 fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
                 lds_barrier();
@@ -1028,6 +1044,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
 }
+
+template __global__ void rx_decode_fused_kernel<0>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2>(RxArgs);
 
 // Frames the fused decode staged but whose final status is not OK: subtract
 // their events from the table (u32 wrap: +1 then -1 leaves every bin exact).

@@ -8,6 +8,7 @@ The workload key is the one bench.py looks up: "<frame_len>:<csum|nocsum>:<frame
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -33,7 +34,7 @@ def load(d: Path):
 def summarise(d: Path) -> dict:
     out = {}
     for k, cs in load(d).items():
-        short = k.split("(")[0].replace("dqdk::", "").replace("void ", "").strip()
+        short = re.sub(r"<[^>]*>", "", k.split("(")[0].replace("dqdk::", "").replace("void ", "")).strip()
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         m["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in m:
