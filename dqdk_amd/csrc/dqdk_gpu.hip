@@ -223,11 +223,23 @@ int hist_flush(dqdk_gpu_queue* q)
 // 4 rounds; 24 with 110 % fill overflowed more than the round saved) and
 // ~115 % at 9000 B (W = 16, 2.85 vs 2.95 ms at W = 12): with every window
 // full of events, fewer rounds win over the keys that overflow to rx_part1.
+//
+// The pieces' runs end mid-line.  Below 128 events per frame (1500 B) the
+// frame loads are non-temporal and the partial lines complete in L2; from
+// 128 on (9000 B: every 2-KB window full of events) whole lines are flushed
+// and remainders carried, which costs stage room, hence the smaller round
+// (A/B, one box, 9000 B: decode 2.86 -> 2.44 ms; at 1500 B lines cost 0.04 ms).
+// policy bit 0: whole-line flushes, bit 1: non-temporal frame loads
+#ifndef DQDK_FUSED_POLICY
+#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 2u)
+#endif
+uint32_t fused_policy(uint32_t E) { return DQDK_FUSED_POLICY; }
+
 uint32_t fused_round_windows(uint32_t E)
 {
     const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
 #ifndef DQDK_FUSED_FILL
-#define DQDK_FUSED_FILL (E >= 128 ? 110 : 80)
+#define DQDK_FUSED_FILL (E >= 128 ? 90 : 80)
 #endif
     const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth
@@ -285,15 +297,13 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         if ((uint64_t)ra.ovf_blk_cap * grid > q->ovf_blk_elems)
             return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
         StageTimer t(q, kStDecode);
-        // non-temporal frame loads below 128 events per frame (A/B: +3 % at
-        // 1500 B, -5 % at 9000 B for the whole path)
-#ifndef DQDK_FUSED_NT_MAX_E
-#define DQDK_FUSED_NT_MAX_E 128
-#endif
-        if (q->E < DQDK_FUSED_NT_MAX_E)
-            hipLaunchKernelGGL(rx_decode_fused_kernel<2>, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
-        else
-            hipLaunchKernelGGL(rx_decode_fused_kernel<0>, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+        // partial-line policy by frame density (fused_policy)
+        const uint32_t pol = fused_policy(q->E);
+        auto kern = pol == 0 ? rx_decode_fused_kernel<0, false>
+                  : pol == 1 ? rx_decode_fused_kernel<0, true>
+                  : pol == 2 ? rx_decode_fused_kernel<2, false>
+                             : rx_decode_fused_kernel<2, true>;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
     } else {
         const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU

@@ -190,7 +190,7 @@ struct HistoArgs {
 };
 
 __global__ void rx_decode_kernel(RxArgs a);
-template <int kLdAux>
+template <int kLdAux, bool kLines>
 __global__ void rx_decode_fused_kernel(RxArgs a);
 __global__ void rx_fixup_kernel(RxArgs a, HistoArgs h);
 __global__ void rx_abort_kernel(CountArgs a);

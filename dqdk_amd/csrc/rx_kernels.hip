@@ -817,14 +817,18 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
 // store is issued (its offset dropped past the run): no dependent chain per
 // bucket and a fixed VMEM pattern.  Rare: keys past a full piece go to the
 // block's overflow region (slot from an LDS counter).
+template <bool kLines>
 __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int lane, uint32_t wave, uint32_t& cur,
-                                            __amdgpu_buffer_rsrc_t ovf_rsrc)
+                                            __amdgpu_buffer_rsrc_t ovf_rsrc, bool last)
 {
     const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
-    uint32_t c = 0, fit = 0;
+    uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
         c = min(lds.scnt[b], (uint32_t)kFCap);
-        fit = min(c, a.piece_cap - cur);
+        // lines mode: whole 128-B lines only (the piece cursor stays line-
+        // aligned, so no store writes part of a line); the rest is carried
+        w = kLines && !last ? (c & ~31u) : c;
+        fit = min(w, a.piece_cap - cur);
     }
     const uint32_t base = cur;
     cur += fit;
@@ -862,10 +866,10 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
             }
         }
     }
-    for (uint64_t m = __ballot(fit < c); m; m &= m - 1) {
+    for (uint64_t m = __ballot(fit < w); m; m &= m - 1) {
         const uint32_t j = (uint32_t)__builtin_ctzll(m);
         const uint32_t bj = wave + (uint32_t)kFWaves * j;
-        const uint32_t fj = rdl(fit, j), nov = rdl(c, j) - fj;
+        const uint32_t fj = rdl(fit, j), nov = rdl(w, j) - fj;
         uint32_t o = 0;
         if (lane == 0)
             o = atomicAdd(&lds.ovf_n, nov);
@@ -873,14 +877,29 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
         for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
             __builtin_amdgcn_raw_buffer_store_b32(lds.stage[bj * kFCap + fj + t], ovf_rsrc, 4u * (o + t), 0, 0);
     }
+    // carry the remainders (< 32 keys, so source and destination do not overlap)
+    for (uint64_t m = kLines ? __ballot(w != 0 && c > w) : 0ull; m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint32_t bj = wave + (uint32_t)kFWaves * j;
+        const uint32_t wj = rdl(w, j), r = rdl(c, j) - wj;
+        uint32_t x = 0;
+        if ((uint32_t)lane < r)
+            x = lds.stage[bj * kFCap + wj + lane];
+        if ((uint32_t)lane < r)
+            lds.stage[bj * kFCap + lane] = x;
+    }
     if (b < (uint32_t)kL1Buckets)
-        lds.scnt[b] = 0;
+        lds.scnt[b] = c - w;
 }
 
-// kLdAux: the frame loads' cache policy (2 = non-temporal: the frames are
-// read once, and keeping them out of L2 leaves it to the pieces' partial
-// lines; measured faster at 1500 B, slower at 9000 B -- the host picks)
-template <int kLdAux>
+// Two policies for the pieces' partial lines (runs end mid-line), chosen by
+// the host per frame density:
+//   kLdAux  the frame loads' cache policy: 2 = non-temporal (the frames are
+//           read once; out of L2 they leave it to the partial lines, which
+//           the next round completes there);
+//   kLines  flush whole 128-B lines only, carrying each bucket's remainder
+//           (< 32 keys) to the next round: no partial line is ever written.
+template <int kLdAux, bool kLines>
 __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 {
     __shared__ FusedLds lds;
@@ -1001,7 +1020,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
 #endif
                 lds_barrier();
-                fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
+                fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, false);
                 lds_barrier();
             }
         }
@@ -1018,7 +1037,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
     // the keys still staged, then the piece sizes for rx_hist_prep
     lds_barrier();
-    fused_flush(a, lds, lane, wave, fcur, ovf_rsrc);
+    fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, true);
     {
         const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
         if (b < (uint32_t)kL1Buckets)
@@ -1045,8 +1064,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
 }
 
-template __global__ void rx_decode_fused_kernel<0>(RxArgs);
-template __global__ void rx_decode_fused_kernel<2>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, true>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, true>(RxArgs);
 
 // Frames the fused decode staged but whose final status is not OK: subtract
 // their events from the table (u32 wrap: +1 then -1 leaves every bin exact).
