@@ -384,7 +384,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             }
             {
                 StageTimer t(q, kStPart2);
-                hipLaunchKernelGGL(rx_part2_kernel, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+                // non-temporal key loads where the fused decode's are (fused_policy bit 1)
+                if (fused_policy(q->E) & 2u)
+                    hipLaunchKernelGGL(rx_part2_kernel<2>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+                else
+                    hipLaunchKernelGGL(rx_part2_kernel<0>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
             }
             HIPCHK(hipGetLastError());
             if (++q->hist_pending == q->hist_k)

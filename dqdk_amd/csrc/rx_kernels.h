@@ -198,6 +198,7 @@ __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);
 __global__ void rx_part1_kernel(HistoArgs a);
 __global__ void rx_hist_prep_kernel(HistoArgs a);
+template <int kLdAux>
 __global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);
 __global__ void rx_slice_heavy_kernel(HistoArgs a);

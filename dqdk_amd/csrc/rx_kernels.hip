@@ -1506,6 +1506,9 @@ __global__ void __launch_bounds__(1024) rx_hist_prep_kernel(HistoArgs a)
 #else
 #define P2_BARRIER lds_barrier
 #endif
+// kLdAux: the key loads' cache policy (2 = non-temporal: each key is read
+// once; measured faster below 128 events per frame, slower from 128 on)
+template <int kLdAux>
 __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
@@ -1584,12 +1587,12 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             }
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], soff[j], 0);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], soff[j], kLdAux);
         } else {
             const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wq0 * 16u + lane) * 4u, j * 256, 0);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wq0 * 16u + lane) * 4u, j * 256, kLdAux);
         }
     };
     uint32_t nk_next = 0;
@@ -1655,6 +1658,9 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         P2_BARRIER();
     }
 }
+
+template __global__ void rx_part2_kernel<0>(HistoArgs);
+template __global__ void rx_part2_kernel<2>(HistoArgs);
 
 // Level 3: one block per 16K-bin slice.  The run offsets of the bucket's
 // items (<= 512 at a time) are staged in LDS first, so gathering a run is
