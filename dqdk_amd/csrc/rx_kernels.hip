@@ -1482,14 +1482,31 @@ __global__ void __launch_bounds__(1024) rx_hist_prep_kernel(HistoArgs a)
     __syncthreads();
     if (tid <= kL1Buckets)
         a.scratch[kOffIstart + tid] = ist[tid * S];
+    // item table: with many items per segment (9000 B: ~126) a wave per
+    // segment, lanes on consecutive items (coalesced stores); with few
+    // (1500 B: ~21) a thread per segment (36 segments per wave in a row
+    // would cost more than the scattered stores)
     uint32_t* items = a.scratch + kOffItems;
-    for (int t = tid; t < nseg; t += 1024) {
-        uint32_t c;
-        uint64_t bs;
-        seg(t, c, bs);
-        for (uint32_t j = 0, it = ist[t]; j * (uint32_t)kPartChunk < c; j++, it++) {
-            items[2 * it] = (uint32_t)((bs + (uint64_t)j * kPartChunk) / kBucketAlign);
-            items[2 * it + 1] = min(c - j * (uint32_t)kPartChunk, (uint32_t)kPartChunk);
+    auto put = [&](uint32_t it, uint64_t bs, uint32_t c, uint32_t j) {
+        items[2 * it] = (uint32_t)((bs + (uint64_t)j * kPartChunk) / kBucketAlign);
+        items[2 * it + 1] = min(c - j * (uint32_t)kPartChunk, (uint32_t)kPartChunk);
+    };
+    if (ist[nseg] > 32u * (uint32_t)nseg) {
+        for (int t = wave; t < nseg; t += 16) {
+            uint32_t c;
+            uint64_t bs;
+            seg(t, c, bs);
+            const uint32_t i0 = ist[t], ni = (c + kPartChunk - 1) / kPartChunk;
+            for (uint32_t j = (uint32_t)lane; j < ni; j += 64)
+                put(i0 + j, bs, c, j);
+        }
+    } else {
+        for (int t = tid; t < nseg; t += 1024) {
+            uint32_t c;
+            uint64_t bs;
+            seg(t, c, bs);
+            for (uint32_t j = 0, it = ist[t]; j * (uint32_t)kPartChunk < c; j++, it++)
+                put(it, bs, c, j);
         }
     }
 }
