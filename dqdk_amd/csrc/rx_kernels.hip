@@ -1564,15 +1564,15 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)b * a.region, a.region * 4u);
             const uint32_t* pr = prow[pb];
             const uint32_t last = a.fgrid - 1;
-            // the piece of the wave's first key (uniform binary search)
+            // the piece of the wave's first key: the number of piece starts
+            // pr[1..fgrid) at or below it (pr is non-decreasing; pr[0] = 0),
+            // by four ballots over the row instead of a dependent search
             const uint32_t p0 = S + wq0 * 16u;
-            uint32_t lo = 0, hi = a.fgrid;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (rfl(pr[mid]) <= p0)
-                    lo = mid;
-                else
-                    hi = mid;
+            uint32_t lo = 0;
+#pragma unroll
+            for (int m = 0; m < (kMaxFusedGrid + 63) / 64; m++) {
+                const uint32_t k = 1u + lane + 64u * (uint32_t)m;
+                lo += (uint32_t)__builtin_popcountll(__ballot(k < a.fgrid && pr[min(k, (uint32_t)kMaxFusedGrid)] <= p0));
             }
             uint32_t cur = rfl(pr[lo]), nxt = rfl(pr[lo + 1]);
             // common case (no piece boundary and no item end inside the load):
