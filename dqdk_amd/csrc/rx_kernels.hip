@@ -347,6 +347,9 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 #ifndef DQDK_ST_AUX
 #define DQDK_ST_AUX 0
 #endif
+#ifndef DQDK_P2ST_AUX  // rx_part2's output stores
+#define DQDK_P2ST_AUX 0
+#endif
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
@@ -1669,9 +1672,17 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
         // stale LDS past nk lands in the bucket's padding (never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;
+#if DQDK_P2ST_AUX
+        // cache policy of the output stores (16 = sc1, write-through: nothing
+        // left dirty in L2 for the kernel-end write-back)
+        const __amdgpu_buffer_rsrc_t drs = uniform_rsrc(a.part2 + base, ((uint64_t)nk + 7u) / 8u * 16u);
+        for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, st4[p]), drs, p * 16u, 0, DQDK_P2ST_AUX);
+#else
         u32x4_t* dst4 = (u32x4_t*)(a.part2 + base);
         for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
             dst4[p] = st4[p];
+#endif
         P2_BARRIER();
     }
 }
