@@ -784,19 +784,21 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
     const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
     const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
     const bool inb = ch < kChannels && hc < kHists;                  // histogram_event's bounds (tristan.c:236-241)
-    bool ov = false;
-    if (e < Ef) {
-        if (inb) {
-            const uint32_t b = key >> kL1Shift;
-            const uint32_t slot = atomicAdd(&lds.scnt[b], 1u);
-            if (slot < (uint32_t)kFCap)
-                lds.stage[b * kFCap + slot] = key;
-            else
-                ov = true;
-        } else {
-            atomicAdd(&lds.oob[oob_slot], 1u);
-        }
-    }
+    // one returning LDS add per event, to the bucket's stage count or to the
+    // frame's out-of-bounds count, and one masked stage store: two masked
+    // operations instead of two levels of divergent branches (decode -2 % at
+    // 1500 B, A/B on one box; the same at 9000 B)
+    const bool has = e < Ef;
+    const uint32_t b = key >> kL1Shift;
+    uint32_t* const cnt = inb ? &lds.scnt[min(b, (uint32_t)kL1Buckets - 1)] : &lds.oob[oob_slot];
+    uint32_t slot = 0;
+    if (has)
+        slot = atomicAdd(cnt, 1u);
+    const bool ink = has && inb;
+    if (ink && slot < (uint32_t)kFCap)
+        lds.stage[b * kFCap + slot] = key;
+    const bool ov = ink && slot >= (uint32_t)kFCap;
+
     // overflow slots: one LDS atomic per wave (lanes ranked by mbcnt), not one
     // per key on the block's single counter (64 lanes on one address serialise)
     uint32_t ooff = kOOB;
