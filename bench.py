@@ -74,6 +74,9 @@ def parse_args(argv=None):
     p.add_argument("--cpu-baseline-sec", type=float, default=8.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--share-gpu", action="store_true",
+                   help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
+                        "collectives over gloo (the data path has none); the numbers are not a scaling result")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_summary.json"),
                    help="rocprofv3 PMC summary used for roofline.traffic")
     return p.parse_args(argv)
@@ -351,7 +354,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                    "mean_frame_len": round(Lm, 1), "stride": stride, "payloadsz": payloadsz,
                    "events_per_frame": E, "csum": not args.no_csum, "histogram": histo,
                    "decode": "fused (keys bucketed in the decode)" if fused else "records",
-                   "parallelism": f"queue-per-gpu x{world}"},
+                   "parallelism": f"queue-per-gpu x{world}" + (" (shared-GPU rehearsal)" if args.share_gpu else "")},
         "frame_GB_s": round(frame_gbs, 2),
         "per_gpu": per_rank,
         "step_ms_median": round(step_ms[len(step_ms) // 2], 4),
@@ -368,6 +371,8 @@ def aggregate_ranks(torch, dist, dev, world, elapsed, t_rank, packets, frame_byt
     from each rank's own time.  Returns (elapsed, per_gpu list or None)."""
     if world == 1:
         return elapsed, None
+    if dist.get_backend() == "gloo":
+        dev = torch.device("cpu")
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     mine = torch.tensor([packets / t_rank / 1e6, frame_bytes / t_rank / 1e9], dtype=torch.float64, device=dev)
@@ -452,7 +457,8 @@ def run_e2e(args, torch, dist, dev, rank, world, local):
         if world > 1:
             dist.barrier()
         r = pl.run(args.steps, rate)
-        t = torch.tensor([r["sec"], r["Mpkt_s"], r["batch_latency_ms"]["p99"]], dtype=torch.float64, device=dev)
+        cdev = torch.device("cpu") if world > 1 and dist.get_backend() == "gloo" else dev
+        t = torch.tensor([r["sec"], r["Mpkt_s"], r["batch_latency_ms"]["p99"]], dtype=torch.float64, device=cdev)
         if world > 1:
             allr = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(allr, t)
@@ -499,6 +505,11 @@ def main():
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
+    elif args.share_gpu:
+        dev = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if world > 1:
+            dist.init_process_group("gloo")  # RCCL refuses two ranks on one GPU
     else:
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)

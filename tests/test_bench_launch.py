@@ -8,6 +8,8 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -44,3 +46,19 @@ def test_world_size_mismatch_is_an_error():
     p = run(["--gpus", "1", "--steps", "2", "--cpu-dry-run"], env={"WORLD_SIZE": "2", "RANK": "0"})
     assert p.returncode == 2
     assert "WORLD_SIZE=2" in p.stderr
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_rehearsal():
+    """The N-rank bench on hardware: `--gpus 2` starts two ranks that each
+    run their own queue on the GPU (shared here: one-GPU box, control plane
+    over gloo), barrier + max over ranks, one line from rank 0."""
+    p = run(["--gpus", "2", "--share-gpu", "--steps", "3", "--warmup", "1", "--frames", "65536", "--no-9000",
+             "--no-cpu-baseline"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and [r["rank"] for r in d["per_gpu"]] == [0, 1]
+    assert all(r["Mpkt_s"] > 0 for r in d["per_gpu"])
+    assert "shared-GPU rehearsal" in d["config"]["parallelism"]
