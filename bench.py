@@ -166,7 +166,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
     frame_bytes = int(desc["len"].astype(np.int64).sum())  # per batch (n * L unless mixed)
     Lm = frame_bytes / n  # mean frame length
-    q = D.RxQueue(local, cfg, n)
+    q = D.RxQueue(dev.index, cfg, n)  # (the rank's GPU: LOCAL_RANK, or LOCAL_RANK % count when shared)
     stream = torch.cuda.current_stream(dev)
     q.set_stream(stream.cuda_stream)
 
@@ -239,7 +239,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
     if histo and E and not pass_records:
         # the frame-order records of this batch, for the statistics below only:
         # a decode-only queue (outside every timed region)
-        with D.RxQueue(local, D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | D.F_NO_HISTO), n) as qr:
+        with D.RxQueue(dev.index, D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | D.F_NO_HISTO), n) as qr:
             qr.set_stream(stream.cuda_stream)
             qr.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
                               d_keys.data_ptr())
@@ -450,7 +450,7 @@ def run_e2e(args, torch, dist, dev, rank, world, local):
     payloadsz = args.payloadsz or (1458 if L == 0 else L - 42)
     cfg = D.RxConfig(payloadsz=payloadsz, mode=D.MODES[args.mode], flags=0 if args.no_csum else D.F_CSUM)
     n = args.e2e_frames
-    pl = E2EPipeline(local, cfg, n, L, stride, queue=rank, depth=3, images=2)
+    pl = E2EPipeline(dev.index, cfg, n, L, stride, queue=rank, depth=3, images=2)
     pl.run(3)  # warm-up
     out = {}
     for name, rate in (("unpaced", None), ("paced", args.offered_gbps * 1e9 / 8 / world)):
