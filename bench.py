@@ -451,7 +451,11 @@ def run_e2e(args, torch, dist, dev, rank, world, local):
     cfg = D.RxConfig(payloadsz=payloadsz, mode=D.MODES[args.mode], flags=0 if args.no_csum else D.F_CSUM)
     n = args.e2e_frames
     pl = E2EPipeline(dev.index, cfg, n, L, stride, queue=rank, depth=3, images=2)
-    pl.run(3)  # warm-up
+
+    def check(b, res, _):
+        assert (res["status"] == D.RX_OK).all(), np.bincount(res["status"])
+
+    pl.run(3, on_result=check)  # warm-up (clean frames: every result OK)
     out = {}
     for name, rate in (("unpaced", None), ("paced", args.offered_gbps * 1e9 / 8 / world)):
         if world > 1:

@@ -11,7 +11,11 @@
  * seeded.  The "faulty" variant injects, per frame at 1/256 each: bad
  * tot_len, bad udp.len, bad UDP checksum, ihl=6 (4 B of IP options), a
  * 42-B frame (datalen 0), a 40-B frame (udplen 6 < 8 -> datalen wraps); and
- * per event at 1/128 each: channel >= 1512, hist_class in {6,7}.
+ * per event at 1/128 each: channel >= 1512, hist_class in {6,7}.  Bit 1 of
+ * `faulty` (DQDK_SYNTH_PEAKED) piles 3 of every 8 events onto four hot bins
+ * (three L1 buckets): the skewed spectra of real detectors, which overflow
+ * the fused decode's LDS stages and per-block pieces.  Checksums are computed
+ * after the events are written, so a peaked frame is still valid.
  *
  * This is input generation only.  It is not on the hot path and computes
  * nothing the GPU path returns.
@@ -52,7 +56,7 @@ enum { F_TOTLEN = 1, F_UDPLEN = 2, F_CSUM = 4, F_OPTS = 8, F_EMPTY = 16, F_SHORT
 
 static uint32_t frame_faults(const dqdk_synth_cfg_t* c, uint64_t rf)
 {
-    if (!c->faulty)
+    if (!(c->faulty & 1u))
         return 0;
     uint32_t f = 0;
     if ((rf & 0xff) == 0)
@@ -106,8 +110,8 @@ static void write_frame(const dqdk_synth_cfg_t* c, uint64_t g, uint8_t* f, uint3
     st16be(ip + 4, (uint16_t)g);
     ip[8] = 64;
     ip[9] = 17;
-    ip[12] = 192; ip[13] = 168; ip[14] = 10; ip[15] = 103; /* udp.c:110 */
-    ip[16] = 192; ip[17] = 168; ip[18] = 10; ip[19] = 1;   /* udp.c:111 */
+    ip[12] = 192; ip[13] = 168; ip[14] = 10; ip[15] = 103; /* udp.c:76 */
+    ip[16] = 192; ip[17] = 168; ip[18] = 10; ip[19] = 1;   /* udp.c:77 */
     if (ihl == 6)
         memset(ip + 20, 1, 4); /* IPOPT_NOP x4 */
     uint8_t* udp = ip + hs;
@@ -129,7 +133,18 @@ static void write_frame(const dqdk_synth_cfg_t* c, uint64_t g, uint8_t* f, uint3
         uint32_t ch = (uint32_t)(((r & 0xffffffffull) * 1512u) >> 32);
         uint32_t energy = (uint32_t)((r >> 32) & 0xffffff);
         uint32_t hc = (uint32_t)((((r >> 56) & 0xff) * 6u) >> 8);
-        if (c->faulty) {
+        if (c->faulty & 2u) {
+            /* hot bins: (ch, hc, energy >> 8) */
+            static const uint32_t hot[4][3] = { { 3, 1, 0x1234 }, { 3, 1, 0x1235 }, { 700, 4, 0xffff }, { 1511, 5, 0 } };
+            const uint32_t pick = (uint32_t)(r2 >> 56) & 7u;
+            if (pick < 3) {
+                const uint32_t* h = hot[((r2 >> 52) & 3u)];
+                ch = h[0];
+                hc = h[1];
+                energy = (h[2] << 8) | (energy & 0xffu);
+            }
+        }
+        if (c->faulty & 1u) {
             if (((r2 >> 32) & 127) == 0)
                 ch = 0xffffu - (uint32_t)((r2 >> 40) & 0xff);
             if (((r2 >> 39) & 127) == 1)

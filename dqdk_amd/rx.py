@@ -248,15 +248,20 @@ def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, d
 SEED = 20261015
 
 
-def synth_cfg(frame_len: int, stride: int, queue: int = 0, faulty: bool = False, seed: int = SEED) -> L.SynthCfg:
-    return L.SynthCfg(seed, queue, frame_len, stride, int(faulty))
+SYNTH_PEAKED = 2  # dqdk_synth_cfg_t.faulty bit 1: skewed spectrum (hot bins)
+
+
+def synth_cfg(frame_len: int, stride: int, queue: int = 0, faulty: bool = False, seed: int = SEED,
+              peaked: bool = False) -> L.SynthCfg:
+    return L.SynthCfg(seed, queue, frame_len, stride, int(bool(faulty)) | (SYNTH_PEAKED if peaked else 0))
 
 
 def synth_umem(n: int, frame_len: int, stride: int, queue: int = 0, faulty: bool = False, seed: int = SEED,
-               first: int = 0, threads: int = 8, pad: int = 0, out: np.ndarray | None = None
+               first: int = 0, threads: int = 8, pad: int = 0, out: np.ndarray | None = None, peaked: bool = False
                ) -> tuple[np.ndarray, np.ndarray]:
-    """Fill a host UMEM image with n synthetic frames; returns (umem u8, desc)."""
-    c = synth_cfg(frame_len, stride, queue, faulty, seed)
+    """Fill a host UMEM image with n synthetic frames; returns (umem u8, desc).
+    faulty: header/checksum/event faults; peaked: 3/8 of the events on four hot bins."""
+    c = synth_cfg(frame_len, stride, queue, faulty, seed, peaked)
     size = int(L.lib().dqdk_synth_umem_size(C.byref(c), n)) + pad
     size = (size + 15) // 16 * 16
     umem = out if out is not None else np.empty(size, dtype=np.uint8)

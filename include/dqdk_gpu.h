@@ -288,8 +288,10 @@ typedef struct dqdk_synth_cfg {
     uint32_t queue;     /* RX queue id: UDP source port 5000+queue           */
     uint32_t frame_len; /* L; 0 = seeded 50/50 mix of 1500 and 9000 B        */
     uint32_t stride;    /* UMEM bytes per frame slot (4096, 9216, ...)       */
-    uint32_t faulty;    /* inject header/checksum/event faults               */
+    uint32_t faulty;    /* bit 0: inject header/checksum/event faults;       */
+                        /* bit 1 (DQDK_SYNTH_PEAKED): skewed spectrum         */
 } dqdk_synth_cfg_t;
+#define DQDK_SYNTH_PEAKED 2u
 
 uint64_t dqdk_synth_umem_size(const dqdk_synth_cfg_t* c, uint32_t n);
 uint32_t dqdk_synth_frame_len(const dqdk_synth_cfg_t* c, uint64_t frame_index);

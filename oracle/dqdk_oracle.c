@@ -588,3 +588,73 @@ double or_rx_batch_threads(uint8_t* umem, uint64_t umem_size, const or_desc_t* d
     free(tid);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---------------------------------------------------------------------- */
+/* or_rx_batch over T threads with identical outputs (full-size checks).   */
+/* ---------------------------------------------------------------------- */
+
+typedef struct {
+    uint8_t* umem;
+    uint64_t umem_size;
+    const or_desc_t* d;
+    uint32_t lo, n;
+    const or_cfg_t* cfg;
+    or_result_t* res;
+    or_counters_t c;
+    uint32_t* hist;
+    uint32_t* keys;
+} mt_arg_t;
+
+static void* mt_main(void* p)
+{
+    mt_arg_t* a = (mt_arg_t*)p;
+    memset(&a->c, 0, sizeof(a->c));
+    uint32_t E = or_events_per_payload(a->cfg->mode, a->cfg->payloadsz);
+    or_rx_batch(a->umem, a->umem_size, a->d + a->lo, a->n, a->cfg, a->res + a->lo, &a->c, a->hist,
+                a->keys ? a->keys + (size_t)a->lo * E : NULL);
+    return NULL;
+}
+
+int or_rx_batch_mt(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, uint32_t n, const or_cfg_t* cfg,
+                   or_result_t* res, or_counters_t* c, uint32_t* hist, uint32_t* keys, int threads)
+{
+    if (threads <= 1 || n < 2 * (uint32_t)threads || (cfg->flags & (OR_F_BATCH_ABORT | OR_F_CSUM_WRITEBACK)))
+        return or_rx_batch(umem, umem_size, d, n, cfg, res, c, hist, keys);
+    if (threads > 64)
+        threads = 64;
+    mt_arg_t args[64];
+    pthread_t tid[64];
+    uint32_t per = (n + (uint32_t)threads - 1) / (uint32_t)threads;
+    for (int t = 0; t < threads; t++) {
+        uint32_t lo = (uint32_t)t * per;
+        uint32_t hi = lo + per > n ? n : lo + per;
+        if (lo > n)
+            lo = n;
+        args[t] = (mt_arg_t){ umem, umem_size, d, lo, hi - lo, cfg, res, { 0 }, hist, keys };
+        pthread_create(&tid[t], NULL, mt_main, &args[t]);
+    }
+    uint64_t first = n;
+    uint64_t failed = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
+        const or_counters_t* x = &args[t].c;
+        c->rcvd_frames += x->rcvd_frames;
+        c->rcvd_pkts += x->rcvd_pkts;
+        c->rcvd_bytes += x->rcvd_bytes;
+        c->invalid_ip_pkts += x->invalid_ip_pkts;
+        c->invalid_udp_pkts += x->invalid_udp_pkts;
+        c->total_events += x->total_events;
+        c->total_bytes += x->total_bytes;
+        c->oob_events += x->oob_events;
+        c->empty_pkts += x->empty_pkts;
+        c->filtered_frames += x->filtered_frames;
+        if (x->failing_batches) {
+            failed = 1;
+            if (args[t].lo + x->first_abort_idx < first)
+                first = args[t].lo + x->first_abort_idx;
+        }
+    }
+    c->failing_batches += failed; /* dqdk.c:317-319: once per batch */
+    c->first_abort_idx = first;
+    return 0;
+}

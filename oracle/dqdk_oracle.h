@@ -153,6 +153,15 @@ double or_rx_batch_threads(uint8_t* umem, uint64_t umem_size, const or_desc_t* d
                            const or_cfg_t* cfg, or_result_t* res, or_counters_t* cnt,
                            uint32_t* hist, int threads);
 
+/* or_rx_batch's exact outputs (results, keys, counters, histogram) for
+ * large batches, computed by T threads over contiguous slices of the
+ * descriptors and merged (counters summed, failing_batches = any failure,
+ * first_abort_idx = the first failing index).  Per-packet accounting only:
+ * with OR_F_BATCH_ABORT or OR_F_CSUM_WRITEBACK (or T <= 1) it runs
+ * or_rx_batch itself.  Test infrastructure for full-size parity checks. */
+int or_rx_batch_mt(uint8_t* umem, uint64_t umem_size, const or_desc_t* d, uint32_t n, const or_cfg_t* cfg,
+                   or_result_t* res, or_counters_t* cnt, uint32_t* hist, uint32_t* keys, int threads);
+
 /*
  * The async consumer (async_processor, tristan.c:332-375) over a ring of
  * nelem elements of payloadsz bytes (post_async's elements, dqdk.c:220-229),

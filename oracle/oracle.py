@@ -84,6 +84,8 @@ def oracle() -> C.CDLL:
         h.or_async_process.restype = C.c_int
         h.or_async_process.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), C.c_int, C.POINTER(Counters), _P, _P, _U64,
                                        C.POINTER(_U64)]
+        h.or_rx_batch_mt.restype = C.c_int
+        h.or_rx_batch_mt.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), _P, C.POINTER(Counters), _P, _P, C.c_int]
         h.or_rx_batch_threads.restype = C.c_double
         h.or_rx_batch_threads.argtypes = [_P, _U64, _P, _U32, C.POINTER(Cfg), _P, C.POINTER(Counters), _P,
                                           C.c_int]
@@ -114,11 +116,13 @@ def events_per_payload(mode: int, payloadsz: int) -> int:
 
 
 def rx_batch(umem: np.ndarray, desc: np.ndarray, payloadsz: int, mode: int = 3, flags: int = 0,
-             port_start: int = 0, port_end: int = 0, want_keys: bool = True, hist: np.ndarray | None = None):
+             port_start: int = 0, port_end: int = 0, want_keys: bool = True, hist: np.ndarray | None = None,
+             threads: int = 1):
     """Run one fetch_xsk batch through the C restatement.
 
     Returns (results, counters dict, keys[n*E] or None).  ``hist`` (u32,
-    HISTO_ENTRIES) is accumulated in place when given.
+    HISTO_ENTRIES) is accumulated in place when given.  threads > 1 splits
+    the frames over host threads with identical outputs (or_rx_batch_mt).
     """
     assert umem.dtype == np.uint8 and umem.flags.c_contiguous
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
@@ -130,9 +134,9 @@ def rx_batch(umem: np.ndarray, desc: np.ndarray, payloadsz: int, mode: int = 3, 
     cfg = Cfg(payloadsz, mode, flags, port_start, port_end)
     if hist is not None:
         assert hist.dtype == np.uint32 and hist.size == HISTO_ENTRIES
-    oracle().or_rx_batch(umem.ctypes.data, umem.nbytes, desc.ctypes.data, n, C.byref(cfg), res.ctypes.data,
-                         C.byref(cnt), hist.ctypes.data if hist is not None else None,
-                         keys.ctypes.data if keys is not None else None)
+    oracle().or_rx_batch_mt(umem.ctypes.data, umem.nbytes, desc.ctypes.data, n, C.byref(cfg), res.ctypes.data,
+                            C.byref(cnt), hist.ctypes.data if hist is not None else None,
+                            keys.ctypes.data if keys is not None else None, threads)
     return res, cnt.as_dict(), keys
 
 

@@ -80,3 +80,31 @@ def test_prefilter_matches_forwarder_rules():
     assert lib.or_prefilter(p, 34, 5000, 5000) == 0  # length checked before protocol
     f[12] = 0x86
     assert lib.or_prefilter(p, 20, 5000, 5000) == 1  # not IPv4: PASS before the ip length check
+
+
+def test_threaded_oracle_equals_sequential():
+    """or_rx_batch_mt (the full-size GPU checks' oracle) == or_rx_batch:
+    results, keys, counters and the table, faulty data, several threads."""
+    umem, desc = D.synth_umem(6000, 1500, 4096, faulty=True)
+    for flags in (0, D.F_CSUM, D.F_CSUM | D.F_PREFILTER):
+        h1 = np.zeros(O.HISTO_ENTRIES, np.uint32)
+        h8 = np.zeros(O.HISTO_ENTRIES, np.uint32)
+        r1, c1, k1 = O.rx_batch(umem.copy(), desc, 1458, flags=flags, port_start=5000, port_end=5000, hist=h1)
+        r8, c8, k8 = O.rx_batch(umem.copy(), desc, 1458, flags=flags, port_start=5000, port_end=5000, hist=h8,
+                                threads=7)
+        assert np.array_equal(r1, r8) and np.array_equal(k1, k8) and c1 == c8, (c1, c8)
+        assert c1["failing_batches"] == 1 and c1["first_abort_idx"] < len(desc)
+        nz = np.flatnonzero(h1)
+        assert np.array_equal(nz, np.flatnonzero(h8)) and np.array_equal(h1[nz], h8[nz])
+
+
+def test_peaked_synth_frames_stay_valid():
+    """DQDK_SYNTH_PEAKED: 3/8 of the events on four hot bins, checksums
+    still valid (computed after the events)."""
+    umem, desc = D.synth_umem(512, 1500, 4096, peaked=True)
+    res, c, keys = O.rx_batch(umem.copy(), desc, 1458, flags=D.F_CSUM)
+    assert (res["status"] == D.RX_OK).all() and c["oob_events"] == 0
+    u, cnt = np.unique(keys, return_counts=True)
+    hot = cnt.argsort()[-4:]
+    assert 0.3 < cnt[hot].sum() / keys.size < 0.45
+    assert len(np.unique(u[hot] >> 21)) == 3  # three L1 buckets

@@ -1,0 +1,150 @@
+"""The benchmarked form at the benchmarked sizes, against the oracle.
+
+bench.py runs histogram batches with NO record buffer: partitioned batches
+then take rx_decode_fused (keys bucketed in the decode's LDS stages and
+appended to per-block pieces, rx_fixup taking back frames that fail the UDP
+checksum afterwards, rx_part2 gathering the pieces), at 1M x 1500 B and
+1M x 9000 B (BASELINE north star) and 256K x 9000 B (configs[2]).  Here the
+same calls run on the same synthetic UMEM and every per-frame result, every
+counter and the WHOLE 2.38 GB table are compared with the oracle
+(or_rx_batch_mt: the C restatement on host threads, identical outputs).
+
+At 1M frames each of the 256 persistent decode blocks iterates four
+super-tiles (rx_kernels.hip, rx_decode_fused_kernel's `st` loop), so the
+piece cursors accumulate across super-tiles; the faulty variants give
+rx_fixup thousands of checksum-failed frames; the peaked variant fills
+the LDS stages and the per-block pieces of three buckets, so keys take the
+overflow path into rx_part1.
+"""
+import numpy as np
+import pytest
+
+import dqdk_amd as D
+from oracle import oracle as O
+from test_gpu_parity import _need_gpu
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+HOST_THREADS = 16  # the GPU box's CPU share
+
+
+def run_bench_form(umem: np.ndarray, desc: np.ndarray, cfg: D.RxConfig, batches: int = 1):
+    """bench.py's step on one queue: device-resident UMEM, no record buffer,
+    flush, then results / counters / table.  Returns (res, counters, table,
+    per-kernel launches)."""
+    _need_gpu()
+    n = len(desc)
+    dev = torch.device("cuda:0")
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_res = torch.full((n * 8,), 0xEE, dtype=torch.uint8, device=dev)
+    with D.RxQueue(0, cfg, n) as q:
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        q.enable_timing(True)
+        for _ in range(batches):
+            q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+        q.flush_histogram()
+        torch.cuda.synchronize()
+        launches = {k: v["launches"] for k, v in q.read_timing().items()}
+        cnt = q.counters()
+        del d_umem, d_desc
+        table = q.histogram()
+    res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
+    return res, cnt, table, launches
+
+
+def oracle_full(umem, desc, cfg):
+    table = np.zeros(D.HISTO_ENTRIES, np.uint32)
+    ores, ocnt, _ = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, want_keys=False, hist=table,
+                               threads=HOST_THREADS)
+    return ores, ocnt, table
+
+
+def assert_same(res, cnt, table, ores, ocnt, otable):
+    assert (res["status"] != 0xEE).all(), "unwritten results"
+    np.testing.assert_array_equal(res["status"], ores["status"])
+    np.testing.assert_array_equal(res["datalen"], ores["datalen"])
+    np.testing.assert_array_equal(res["payload_off"], ores["payload_off"])
+    np.testing.assert_array_equal(res["oob_events"], ores["oob_events"])
+    assert cnt == ocnt, (cnt, ocnt)
+    if not np.array_equal(table, otable):
+        bad = np.flatnonzero(table != otable)
+        raise AssertionError(f"{len(bad)} bins differ, first {bad[:8]}: gpu {table[bad[:8]]} oracle {otable[bad[:8]]}")
+
+
+FULL = [
+    # (frames, L, stride, payloadsz, faulty)
+    (1 << 20, 1500, 4096, 1458, False),   # the default bench line, exactly
+    (1 << 20, 9000, 9216, 8958, False),   # its by_frame_len["9000"]
+    (1 << 18, 9000, 9216, 8958, False),   # configs[2] at its own batch
+    (1 << 20, 1500, 4096, 1458, True),
+    (1 << 20, 9000, 9216, 8958, True),
+]
+
+
+@pytest.mark.parametrize("n,L,stride,payloadsz,faulty", FULL,
+                         ids=["1M-1500-clean", "1M-9000-clean", "256K-9000-clean", "1M-1500-faulty",
+                              "1M-9000-faulty"])
+def test_fused_full_size_vs_oracle(n, L, stride, payloadsz, faulty):
+    umem, desc = D.synth_umem(n, L, stride, faulty=faulty, threads=HOST_THREADS)
+    cfg = D.RxConfig(payloadsz=payloadsz, flags=D.F_CSUM)  # bench.py's flags: auto histogram path
+    res, cnt, table, launches = run_bench_form(umem, desc, cfg)
+    assert launches.get("rx_fixup", 0) == 1, launches  # the fused decode ran (rx_fixup is fused-only)
+    ores, ocnt, otable = oracle_full(umem, desc, cfg)
+    assert_same(res, cnt, table, ores, ocnt, otable)
+    if faulty:
+        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 1000  # rx_fixup takes these back
+        assert ocnt["oob_events"] > 0
+    else:
+        assert (ores["status"] == D.RX_OK).all()
+
+
+def test_fused_peaked_faulty_overflows_pieces():
+    """1M x 1500 B, faulty headers and checksums AND a peaked spectrum (3/8
+    of the events on four hot bins in three L1 buckets): the LDS stages of
+    those buckets overflow every round and their per-block pieces fill, so
+    keys go through the block overflow regions into rx_part1; bins receive
+    far more than 65535 events (rx_slice_heavy's u32 form).  Two batches:
+    the second adds onto the first in the table."""
+    n = 1 << 20
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, peaked=True, threads=HOST_THREADS)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
+    res, cnt, table, launches = run_bench_form(umem, desc, cfg, batches=2)
+    assert launches.get("rx_fixup", 0) == 2 and launches.get("rx_slice_heavy", 0) >= 1, launches
+    ores, ocnt, otable = oracle_full(umem, desc, cfg)
+    otable *= 2
+    ocnt = {k: (v if k == "first_abort_idx" else 2 * v) for k, v in ocnt.items()}
+    assert_same(res, cnt, table, ores, ocnt, otable)
+    assert int(otable.max()) > 0xFFFF
+
+
+def test_records_path_full_size_vs_oracle():
+    """The records path (frame-order 4-B records, rx_part1 grouping them) at
+    1M x 1500 B: every result, record, counter and the whole table."""
+    _need_gpu()
+    n = 1 << 20
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, threads=HOST_THREADS)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
+    E = cfg.events
+    dev = torch.device("cuda:0")
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_res = torch.full((n * 8,), 0xEE, dtype=torch.uint8, device=dev)
+    d_keys = torch.full((n * E,), -1, dtype=torch.int32, device=dev)
+    with D.RxQueue(0, cfg, n) as q:
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), d_keys.data_ptr())
+        torch.cuda.synchronize()
+        cnt = q.counters()
+        del d_umem, d_desc
+        table = q.histogram()
+    res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
+    keys = d_keys.cpu().numpy().view(np.uint32)
+    otable = np.zeros(D.HISTO_ENTRIES, np.uint32)
+    ores, ocnt, okeys = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, hist=otable,
+                                   threads=HOST_THREADS)
+    assert_same(res, cnt, table, ores, ocnt, otable)
+    ok = ores["status"] == D.RX_OK
+    np.testing.assert_array_equal(keys.reshape(n, E)[ok], okeys.reshape(n, E)[ok])
