@@ -10,6 +10,7 @@
  */
 #include <errno.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -45,6 +46,29 @@ int fail_errno(int err, const char* what)
         if (e_ != hipSuccess)               \
             return fail(#x, e_);            \
     } while (0)
+
+// Entry points make the queue's device current and restore the caller's on
+// return (the calling thread's current device is not changed by the ABI).
+struct DevGuard {
+    int prev = -1;
+    hipError_t e;
+    explicit DevGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        e = prev == dev ? hipSuccess : hipSetDevice(dev);
+    }
+    ~DevGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev)
+            (void)hipSetDevice(prev);
+    }
+};
+#define SETDEV(dev)                                   \
+    DevGuard dev_guard_(dev);                         \
+    if (dev_guard_.e != hipSuccess)                   \
+        return fail("hipSetDevice", dev_guard_.e)
 
 constexpr int kStages = DQDK_GPU_TIMING_STAGES;
 enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy, kStFixup };
@@ -114,10 +138,22 @@ struct dqdk_gpu_queue {
     // raw payload stream (tristan.c:318-324)
     int raw_fd = -1;
     uint64_t* d_raw_blk = nullptr;  // per-256-frame byte totals -> offsets
-    uint8_t* d_raw = nullptr;       // host drop-in staging
-    uint64_t raw_cap = 0;
-    uint8_t* h_raw = nullptr;       // pinned
-    uint64_t h_raw_cap = 0;
+    // Host drop-in raw egress, double-buffered: batch b gathers its stream
+    // into d_rawb[b & 1] on the queue stream, the D2H runs on raw_stream into
+    // pinned h_rawb[b & 1], and its write() happens during the next batch's
+    // call, while that batch's kernels run (or at the drain: queue_sync,
+    // set_raw_fd, destroy).
+    hipStream_t raw_stream = nullptr;
+    hipEvent_t raw_ev_d2h[2] = {nullptr, nullptr};
+    uint8_t* d_rawb[2] = {nullptr, nullptr};
+    uint64_t d_rawb_cap[2] = {0, 0};
+    uint8_t* h_rawb[2] = {nullptr, nullptr};
+    uint64_t h_rawb_cap[2] = {0, 0};
+    uint64_t raw_pend_len[2] = {0, 0};
+    int raw_pend[2] = {0, 0};
+    uint64_t raw_seq = 0;
+    uint64_t* h_raw_total = nullptr;  // pinned: the batch's stream length
+    int raw_sync = 0;                 // DQDK_GPU_RAW_SYNC=1: serial gather -> copy -> write() (A/B only)
     // async consumer: per-burst first element / length / output offset
     uint32_t* d_async = nullptr;
     size_t async_cap = 0;  // bursts
@@ -469,37 +505,10 @@ int raw_total(dqdk_gpu_queue* q, uint32_t n, uint64_t* total)
     return 0;
 }
 
-// Host drop-in: append the batch's raw payload stream to q->raw_fd.
-int write_raw(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint32_t n)
+int write_fd(int fd, const uint8_t* p, uint64_t n)
 {
-    int rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, nullptr, 0, false);
-    uint64_t total = 0;
-    if (!rc)
-        rc = raw_total(q, n, &total);
-    if (rc || !total)
-        return rc;
-    if (total > q->raw_cap) {
-        (void)hipFree(q->d_raw);
-        q->d_raw = nullptr;
-        q->raw_cap = 0;
-        HIPCHK(hipMalloc(&q->d_raw, total));
-        q->raw_cap = total;
-    }
-    if (total > q->h_raw_cap) {
-        if (q->h_raw)
-            (void)hipHostFree(q->h_raw);
-        q->h_raw = nullptr;
-        q->h_raw_cap = 0;
-        HIPCHK(hipHostMalloc(&q->h_raw, total, hipHostMallocDefault));
-        q->h_raw_cap = total;
-    }
-    rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, q->d_raw, q->raw_cap, true);
-    if (rc)
-        return rc;
-    HIPCHK(hipMemcpyAsync(q->h_raw, q->d_raw, total, hipMemcpyDeviceToHost, q->stream));
-    HIPCHK(hipStreamSynchronize(q->stream));
-    for (uint64_t o = 0; o < total;) {
-        const ssize_t w = write(q->raw_fd, q->h_raw + o, total - o);
+    for (uint64_t o = 0; o < n;) {
+        const ssize_t w = write(fd, p + o, n - o > (1u << 30) ? (1u << 30) : (size_t)(n - o));
         if (w < 0) {
             if (errno == EINTR)
                 continue;
@@ -510,6 +519,71 @@ int write_raw(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint
         o += (uint64_t)w;
     }
     return 0;
+}
+
+int grow_dev(uint8_t** p, uint64_t* cap, uint64_t need)
+{
+    if (need <= *cap)
+        return 0;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipMalloc(p, need));
+    *cap = need;
+    return 0;
+}
+
+int grow_host(uint8_t** p, uint64_t* cap, uint64_t need)
+{
+    if (need <= *cap)
+        return 0;
+    if (*p)
+        (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipHostMalloc(p, need, hipHostMallocDefault));
+    *cap = need;
+    return 0;
+}
+
+// write() the raw stream of buffer k once its D2H has landed
+int raw_write_pending(dqdk_gpu_queue* q, int k)
+{
+    if (!q->raw_pend[k])
+        return 0;
+    q->raw_pend[k] = 0;
+    HIPCHK(hipEventSynchronize(q->raw_ev_d2h[k]));
+    return write_fd(q->raw_fd, q->h_rawb[k], q->raw_pend_len[k]);
+}
+
+// every batch's raw stream written (older buffer first)
+int raw_drain(dqdk_gpu_queue* q)
+{
+    const int last = (int)((q->raw_seq + 1) & 1);  // buffer of the most recent batch
+    int rc = raw_write_pending(q, last ^ 1);
+    if (!rc)
+        rc = raw_write_pending(q, last);
+    return rc;
+}
+
+// Serial form (DQDK_GPU_RAW_SYNC=1, kept for the A/B): size query, gather,
+// D2H and write() of the batch, all before returning.
+int write_raw_sync(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint32_t n)
+{
+    int rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, nullptr, 0, false);
+    uint64_t total = 0;
+    if (!rc)
+        rc = raw_total(q, n, &total);
+    if (rc || !total)
+        return rc;
+    if ((rc = grow_dev(&q->d_rawb[0], &q->d_rawb_cap[0], total)) || (rc = grow_host(&q->h_rawb[0], &q->h_rawb_cap[0], total)))
+        return rc;
+    rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, q->d_rawb[0], q->d_rawb_cap[0], true);
+    if (rc)
+        return rc;
+    HIPCHK(hipMemcpyAsync(q->h_rawb[0], q->d_rawb[0], total, hipMemcpyDeviceToHost, q->stream));
+    HIPCHK(hipStreamSynchronize(q->stream));
+    return write_fd(q->raw_fd, q->h_rawb[0], total);
 }
 
 }  // namespace
@@ -548,7 +622,7 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail_errno(-ENODEV, "queue_create: device is not gfx950 (MI355X)");
-    HIPCHK(hipSetDevice(device));
+    SETDEV(device);
 
     dqdk_gpu_queue* q = new dqdk_gpu_queue();
     q->device = device;
@@ -559,6 +633,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                (cfg->mode == DQDK_MODE_LISTWAVE || cfg->mode == DQDK_MODE_LISTMODE ||
                 cfg->mode == DQDK_MODE_ENERGYHISTO);  // is_store_histo, src/tristan.c:65-70
     q->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* rs = getenv("DQDK_GPU_RAW_SYNC"))
+        q->raw_sync = atoi(rs) != 0;
     if (cfg->flags & DQDK_GPU_F_HISTO_ATOMIC)
         q->histo_path = 1;
     else if (cfg->flags & DQDK_GPU_F_HISTO_PARTITIONED)
@@ -591,18 +667,16 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
             // Stage up to kHistKMax batches per slice pass, as many as keep a
-            // slice of uniformly spread events at half the 65535 events of the
-            // packed-u16 form (the low-byte sweep is amortised over them; a
-            // fuller slice still takes the u32 form); DQDK_GPU_F_HISTO_EAGER:
-            // a pass per batch.
+            // slice of uniformly spread events at about 3/4 of the 65535
+            // events of the packed-u16 form (kHistSliceEvents; the low-byte
+            // sweep is amortised over them, a fuller slice still takes the u32
+            // form); DQDK_GPU_F_HISTO_EAGER: a pass per batch.
             const size_t per_slice = (nk + kSlices - 1) / kSlices;
             q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
                             ? 1u
                             : (uint32_t)std::max<size_t>(
                                   1, std::min<size_t>(kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1)));
-            // slots start 16-B aligned (part2's 16-B stores and the slice gather's
-            // dword loads assume it): strides rounded to 8 u16 elements
-            // part1/part2: the fused decode's segments, then rx_part1's region
+            // part1/part2 hold the fused decode's pieces, then rx_part1's region
             // (records / overflow); slots start 16-B aligned (part2's 16-B
             // stores and the slice gather's dword loads assume it)
             q->nk_max = nk;
@@ -639,7 +713,9 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
 {
     if (!q)
         return -EINVAL;
-    (void)hipSetDevice(q->device);
+    DevGuard dev_guard_(q->device);
+    if (q->raw_fd >= 0)
+        (void)raw_drain(q);  // the last batch's raw stream still goes to its file
     if (q->stream)
         (void)hipStreamSynchronize(q->stream);
     for (auto& r : q->regs)
@@ -665,9 +741,17 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     (void)hipFree(q->d_raw_blk);
-    (void)hipFree(q->d_raw);
-    if (q->h_raw)
-        (void)hipHostFree(q->h_raw);
+    for (int k = 0; k < 2; k++) {
+        (void)hipFree(q->d_rawb[k]);
+        if (q->h_rawb[k])
+            (void)hipHostFree(q->h_rawb[k]);
+        if (q->raw_ev_d2h[k])
+            (void)hipEventDestroy(q->raw_ev_d2h[k]);
+    }
+    if (q->h_raw_total)
+        (void)hipHostFree(q->h_raw_total);
+    if (q->raw_stream)
+        (void)hipStreamDestroy(q->raw_stream);
     if (q->switch_ev)
         (void)hipEventDestroy(q->switch_ev);
     (void)hipFree(q->d_async);
@@ -686,7 +770,7 @@ int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* s)
         return 0;
     // work already enqueued on the old stream (a batch, staged slice passes)
     // is ordered before anything enqueued on the new one
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (!q->switch_ev)
         HIPCHK(hipEventCreateWithFlags(&q->switch_ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(q->switch_ev, q->stream));
@@ -711,7 +795,7 @@ int dqdk_gpu_rx_batch_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_
         return fail_errno(-EINVAL, "rx_batch_device: umem_size must be a multiple of 16");
     if (n == 0)
         return 0;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     return launch_batch(q, d_umem, umem_size, d_desc, n, d_results, d_keys);
 }
 
@@ -719,7 +803,9 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q)
 {
     if (!q)
         return -EINVAL;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
+    if (int rc = raw_drain(q))
+        return rc;
     HIPCHK(hipStreamSynchronize(q->stream));
     return 0;
 }
@@ -728,7 +814,7 @@ int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size)
 {
     if (!q || !umem || !size)
         return -EINVAL;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     for (auto& r : q->regs)
         if (r.host == umem)
             return 0;
@@ -749,7 +835,7 @@ int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem)
         return -EINVAL;
     for (size_t k = 0; k < q->regs.size(); k++) {
         if (q->regs[k].host == umem) {
-            HIPCHK(hipSetDevice(q->device));
+            SETDEV(q->device);
             HIPCHK(hipStreamSynchronize(q->stream));
             HIPCHK(hipHostUnregister(umem));
             q->regs.erase(q->regs.begin() + (long)k);
@@ -773,7 +859,7 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
             memset(delta, 0, sizeof(*delta));
         return 0;
     }
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     const Reg* reg = nullptr;
     for (auto& r : q->regs)
         if ((const uint8_t*)r.host <= umem && umem + umem_size <= (const uint8_t*)r.host + r.size)
@@ -789,14 +875,64 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
     int rc = launch_batch(q, dev_umem, umem_size, q->d_desc, n, q->d_res, nullptr);
     if (rc)
         return rc;
-    if (q->raw_fd >= 0 && (rc = write_raw(q, dev_umem, umem_size, n)) != 0)
+    const bool raw = q->raw_fd >= 0 && !q->raw_sync;
+    const int k = (int)(q->raw_seq & 1);
+    uint64_t cap = 0;
+    if (raw) {
+        // the batch's raw stream (tristan.c:318-324) is gathered into buffer k
+        // now (the frames are valid only until this call returns, dqdk.c:300);
+        // capacity: the frames' bytes (a payload lies inside its frame unless
+        // its datalen wrapped, handled below by a second gather)
+        if (!q->raw_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&q->raw_stream, hipStreamNonBlocking));
+            for (int j = 0; j < 2; j++)
+                HIPCHK(hipEventCreateWithFlags(&q->raw_ev_d2h[j], hipEventDisableTiming));
+            HIPCHK(hipHostMalloc(&q->h_raw_total, sizeof(uint64_t), hipHostMallocDefault));
+        }
+        uint64_t guess = 0;
+        for (uint32_t i = 0; i < n; i++)
+            guess += d[i].len;
+        if ((rc = grow_dev(&q->d_rawb[k], &q->d_rawb_cap[k], std::max<uint64_t>(guess, 4096))) != 0)
+            return rc;
+        cap = q->d_rawb_cap[k];
+        if ((rc = launch_raw(q, dev_umem, umem_size, q->d_desc, n, q->d_res, q->d_rawb[k], cap, true)) != 0)
+            return rc;
+        const uint32_t nblk = (n + kRawThreads - 1) / kRawThreads;
+        HIPCHK(hipMemcpyAsync(q->h_raw_total, q->d_raw_blk + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              q->stream));
+    } else if (q->raw_fd >= 0 && (rc = write_raw_sync(q, dev_umem, umem_size, n)) != 0) {
         return rc;
+    }
     HIPCHK(hipMemcpyAsync(per_pkt, q->d_res, (size_t)n * sizeof(*per_pkt), hipMemcpyDeviceToHost, q->stream));
     uint64_t b[kBatchScratch];
     HIPCHK(hipMemcpyAsync(b, q->d_batch, sizeof(b), hipMemcpyDeviceToHost, q->stream));
+    // the previous batch's raw stream goes to its file while this batch runs
+    if (raw && (rc = raw_write_pending(q, k ^ 1)) != 0)
+        return rc;
     HIPCHK(hipStreamSynchronize(q->stream));
     if (delta)
         memcpy(delta, &b[1], sizeof(*delta));
+    if (raw) {
+        const uint64_t total = *q->h_raw_total;
+        if (total > cap) {  // wrapped datalen inside the UMEM: gather again at full size
+            if ((rc = grow_dev(&q->d_rawb[k], &q->d_rawb_cap[k], total)) != 0 ||
+                (rc = launch_raw(q, dev_umem, umem_size, q->d_desc, n, q->d_res, q->d_rawb[k], total, true)) != 0)
+                return rc;
+        }
+        if (total) {
+            if ((rc = grow_host(&q->h_rawb[k], &q->h_rawb_cap[k], total)) != 0)
+                return rc;
+            HIPCHK(hipEventRecord(q->raw_ev_d2h[k], q->stream));  // after the gather
+            HIPCHK(hipStreamWaitEvent(q->raw_stream, q->raw_ev_d2h[k], 0));
+            HIPCHK(hipMemcpyAsync(q->h_rawb[k], q->d_rawb[k], total, hipMemcpyDeviceToHost, q->raw_stream));
+            HIPCHK(hipEventRecord(q->raw_ev_d2h[k], q->raw_stream));
+            q->raw_pend[k] = 1;
+            q->raw_pend_len[k] = total;
+        }
+        if (total > cap)  // the second gather read the frames: done before returning
+            HIPCHK(hipStreamSynchronize(q->stream));
+        q->raw_seq++;
+    }
     return 0;
 }
 
@@ -804,7 +940,7 @@ int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out)
 {
     if (!q || !out)
         return -EINVAL;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     HIPCHK(hipMemcpyAsync(out, q->d_cum, sizeof(*out), hipMemcpyDeviceToHost, q->stream));
     HIPCHK(hipStreamSynchronize(q->stream));
     return 0;
@@ -814,7 +950,7 @@ int dqdk_gpu_counters_reset(dqdk_gpu_queue_t* q)
 {
     if (!q)
         return -EINVAL;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     HIPCHK(hipMemsetAsync(q->d_cum, 0, sizeof(dqdk_gpu_counters_t), q->stream));
     return 0;
 }
@@ -825,7 +961,7 @@ int dqdk_gpu_histogram_get(dqdk_gpu_queue_t* q, uint32_t* host_hist)
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_get: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (int rc = hist_flush(q))
         return rc;
     return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
@@ -839,7 +975,7 @@ int dqdk_gpu_histogram_accumulate(dqdk_gpu_queue_t* q, uint32_t* host_hist)
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_accumulate: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (int rc = hist_flush(q))
         return rc;
     return stream_table(q, [&](const uint32_t* h, uint64_t o, uint64_t m) {
@@ -854,7 +990,7 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q)
         return -EINVAL;
     if (!q->d_hist)
         return 0;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     q->hist_pending = 0;  // staged batches are dropped with the table
     HIPCHK(hipMemsetAsync(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->stream));
     HIPCHK(hipMemsetAsync(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES, q->stream));
@@ -865,7 +1001,8 @@ uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q)
 {
     if (!q || !q->d_hist)
         return nullptr;
-    if (hipSetDevice(q->device) != hipSuccess)
+    DevGuard dev_guard_(q->device);
+    if (dev_guard_.e != hipSuccess)
         return nullptr;
     if (!q->d_snap && hipMalloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t)) != hipSuccess) {
         q->d_snap = nullptr;
@@ -897,7 +1034,7 @@ int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts
 {
     if (!q)
         return -EINVAL;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     HIPCHK(hipStreamSynchronize(q->stream));
     for (auto& p : q->pending) {
         float ms = 0.f;
@@ -932,7 +1069,7 @@ int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint
             *total = 0;
         return 0;
     }
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     int rc = launch_raw(q, d_umem, umem_size, d_desc, n, d_results, d_out, out_cap, d_out != nullptr);
     if (!rc && total)
         rc = raw_total(q, n, total);
@@ -966,7 +1103,7 @@ int dqdk_gpu_async_process_device(dqdk_gpu_queue_t* q, const uint8_t* d_ring, ui
         *total = off;
     if (nbursts == 0)
         return 0;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (q->async_cap < nbursts) {
         HIPCHK(hipStreamSynchronize(q->stream));
         (void)hipFree(q->d_async);
@@ -1001,6 +1138,11 @@ int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)
 {
     if (!q)
         return -EINVAL;
+    if (q->raw_fd >= 0 && fd != q->raw_fd) {  // what went to the old fd is written there first
+        SETDEV(q->device);
+        if (int rc = raw_drain(q))
+            return rc;
+    }
     q->raw_fd = fd;
     return 0;
 }
@@ -1013,7 +1155,7 @@ int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q)
         return -EINVAL;
     if (!q->d_hist)
         return 0;
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     return hist_flush(q);
 }
 
@@ -1023,7 +1165,7 @@ int dqdk_gpu_histogram_copy(dqdk_gpu_queue_t* q, uint32_t* d_dst)
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_copy: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (int rc = hist_flush(q))
         return rc;
     return combine(q, d_dst, 0, DQDK_TRISTAN_HISTO_ENTRIES);
@@ -1035,7 +1177,7 @@ int dqdk_gpu_histogram_add(dqdk_gpu_queue_t* q, const uint32_t* d_src)
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_add: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     const uint64_t n16 = DQDK_TRISTAN_HISTO_ENTRIES / 4;
     hipLaunchKernelGGL(hist_add_kernel, dim3((uint32_t)q->cu_count * 8u), dim3(256), 0, q->stream, q->d_hist, d_src, n16);
     HIPCHK(hipGetLastError());
@@ -1048,7 +1190,7 @@ int dqdk_gpu_histogram_nonzero(dqdk_gpu_queue_t* q, uint64_t* count)
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_nonzero: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (int rc = hist_flush(q))
         return rc;
     unsigned long long* d = nullptr;
@@ -1098,7 +1240,7 @@ int dqdk_gpu_histogram_write_csv(dqdk_gpu_queue_t* q, int fd, uint64_t* bytes_wr
         return -EINVAL;
     if (!q->d_hist)
         return fail_errno(-ENOENT, "histogram_write_csv: queue has no histogram");
-    HIPCHK(hipSetDevice(q->device));
+    SETDEV(q->device);
     if (int rc = hist_flush(q))
         return rc;
     static const char header[] = "Channel,Histo,Energy,Freq\n";  // src/tristan.c:198

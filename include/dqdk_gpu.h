@@ -136,7 +136,11 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
 int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q);
 /* Queues start on a stream of their own (hipStreamNonBlocking).  Run the
  * queue's work on the caller's hipStream_t instead -- verbatim, so NULL is
- * the legacy default stream -- to order it after the caller's producers. */
+ * the legacy default stream -- to order it after the caller's producers.
+ * Work already enqueued on the current stream is ordered before the new
+ * one's (an event is recorded on it), so the current stream must still be
+ * alive at the switch: switch away before destroying a caller stream.
+ * No entry point changes the calling thread's current HIP device. */
 int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* hip_stream);
 void* dqdk_gpu_queue_stream(dqdk_gpu_queue_t* q);     /* current stream     */
 void* dqdk_gpu_queue_own_stream(dqdk_gpu_queue_t* q); /* the queue's own one */
@@ -171,12 +175,17 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
  * with the same d_desc/d_results; writes min(total, out_cap) bytes to d_out
  * (NULL with out_cap 0 = size query).  total (host, nullable) = the stream's
  * full length, which makes the call synchronous.  Host form: with a raw fd
- * set, dqdk_gpu_rx_batch appends each batch's stream to it (GPU gather, one
- * D2H copy, write()). */
+ * set, dqdk_gpu_rx_batch appends each batch's stream to it: the GPU gathers
+ * the stream before the call returns (the frames are valid only until the
+ * descriptors are released, src/dqdk.c:300), its D2H copy runs on a side
+ * stream into one of two pinned buffers, and its write() happens during the
+ * next dqdk_gpu_rx_batch call while that batch's kernels run -- or at
+ * dqdk_gpu_queue_sync, dqdk_gpu_queue_set_raw_fd and dqdk_gpu_queue_destroy,
+ * which drain it.  A failed write() is returned by the call that makes it. */
 int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
                                 const dqdk_gpu_desc_t* d_desc, uint32_t n, const dqdk_gpu_rx_result_t* d_results,
                                 uint8_t* d_out, uint64_t out_cap, uint64_t* total);
-int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd); /* -1 = off (default) */
+int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd); /* -1 = off (default); drains first */
 
 /* ---- async consumer (async_processor, src/tristan.c:332-375) --------------- */
 /* The raw/async modes hand each payload to post_async (src/dqdk.c:220-229):

@@ -269,3 +269,39 @@ def test_raw_stream_host_dropin_appends_to_fd(tmp_path):
         q.close()
         os.close(fd)
     assert path.read_bytes() == b"".join(want)
+
+
+def test_raw_stream_side_stream_multi_batch(tmp_path):
+    """Host drop-in raw egress over 8 batches of varying size: each batch's
+    stream is gathered before the call returns, copied D2H on a side stream
+    into one of two pinned buffers and written during the next call; the
+    file is complete after queue_sync (drain) and after destroy without a
+    set_raw_fd(-1).  Byte-equal to the oracle's concatenation."""
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM)
+    path = tmp_path / "raw.bin"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    want = []
+    sizes = [512, 4096, 1024, 8192, 64, 8192, 2048, 3000]
+    try:
+        q = D.RxQueue(0, cfg, max(sizes))
+        try:
+            q.set_raw_fd(fd)
+            for b, n in enumerate(sizes):
+                L = 9000 if b % 3 == 1 else 1500
+                umem, desc = D.synth_umem(n, L, 9216, queue=b, faulty=True)
+                res, _ = q.process_batch(umem, desc)
+                ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+                np.testing.assert_array_equal(res, ores)
+                want.append(ref_raw(umem, desc, ores, ocnt, cfg.flags))
+                umem[:] = 0xCD  # the caller may reuse its frames once the call returned (dqdk.c:300)
+                q.unregister_umem(umem)
+                if b == 3:
+                    q.sync()  # drains: everything so far is in the file
+                    assert path.read_bytes() == b"".join(want)
+            assert len(path.read_bytes()) < sum(map(len, want))  # the last batch is still in flight
+        finally:
+            q.close()  # drains the last batch into the still-open fd
+        assert path.read_bytes() == b"".join(want)
+    finally:
+        os.close(fd)

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Host drop-in raw egress rate (dqdk_gpu_rx_batch with a raw fd): the serial
+form (gather -> D2H -> write() inside each call, DQDK_GPU_RAW_SYNC=1) against
+the side-stream form (D2H on a side stream, write() of batch b during batch
+b+1's call).  Waveform mode (the raw-storing mode, src/tristan.c:318-324),
+1500 B frames, registered host UMEM, the file in /tmp.  Prints one JSON line."""
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import dqdk_amd as D  # noqa: E402
+
+
+def rate(sync: bool, n: int, batches: int, mode: int) -> dict:
+    os.environ["DQDK_GPU_RAW_SYNC"] = "1" if sync else "0"
+    cfg = D.RxConfig(payloadsz=1458, mode=mode, flags=D.F_CSUM)
+    imgs = [D.synth_umem(n, 1500, 4096, queue=k, threads=16) for k in range(2)]
+    fd, path = tempfile.mkstemp(dir="/tmp")
+    try:
+        with D.RxQueue(0, cfg, n) as q:
+            for u, _ in imgs:
+                q.register_umem(u)
+            q.set_raw_fd(fd)
+            q.process_batch(*imgs[0])
+            q.sync()
+            t0 = time.perf_counter()
+            for b in range(batches):
+                q.process_batch(*imgs[b % 2])
+            q.sync()
+            sec = time.perf_counter() - t0
+            q.set_raw_fd(-1)
+        size = os.path.getsize(path)
+    finally:
+        os.close(fd)
+        os.unlink(path)
+    assert size == (batches + 1) * n * 1458, size
+    return {"Mpkt_s": round(n * batches / sec / 1e6, 3), "raw_GB_s": round(n * 1458 * batches / sec / 1e9, 3)}
+
+
+def main():
+    n, batches = 1 << 16, 24
+    out = {"frames_per_batch": n, "batches": batches, "frame_len": 1500}
+    for mode_name, mode in (("waveform", D.MODE_WAVEFORM), ("listmode", D.MODE_LISTMODE)):
+        out[mode_name] = {"serial": rate(True, n, batches, mode), "side_stream": rate(False, n, batches, mode)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
