@@ -159,6 +159,32 @@ __global__ __launch_bounds__(256) void copy11_kernel(const u32x4_t* __restrict__
     }
 }
 
+// Write calibration for rocprofv3's WRITE_SIZE (MI355X_MICROARCH.md: exact
+// only for 16-B-per-lane streaming stores): 4-B-per-lane stores of a known
+// byte count.  runs == 0: every wave instruction writes 64 consecutive dwords
+// (256 B, line-aligned); runs > 0: the fused decode's piece-flush shape --
+// each wave instruction writes a run of `runs` (< 64) dwords starting at a
+// dword offset that is not line-aligned, runs of one block following each
+// other inside a private region (as a piece fills over rounds).
+// Bytes written = n * (runs ? runs : 64) * 4.
+__global__ __launch_bounds__(256) void store_b32_kernel(uint32_t* __restrict__ out, uint32_t n, uint32_t runs)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4;
+    const uint32_t w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t per = runs ? runs : 64u;
+    // wave w writes instructions w, w + nw, ... ; with runs its instructions'
+    // runs are adjacent in its own region (a piece), starting 13 dwords in
+    const uint64_t region = ((uint64_t)(n / nw + 1) * per + 64) & ~31ull;
+    uint64_t cur = runs ? (uint64_t)w0 * region + 13 : 0;
+    for (uint32_t i = w0; i < n; i += nw) {
+        const uint64_t o = runs ? cur : (uint64_t)i * 64;
+        if (lane < per)
+            out[o + lane] = i ^ lane;  // plain stores, as the piece flush
+        cur += per;
+    }
+}
+
 int timed(hipStream_t s, int iters, float* ms, void (*launch)(hipStream_t, const void*), const void* ctx)
 {
     hipEvent_t a, b;
@@ -207,7 +233,9 @@ struct FramesCtx {
 void launch_frames(hipStream_t s, const void* c)
 {
     const FramesCtx* r = (const FramesCtx*)c;
-    if (r->flat == 4)
+    if (r->flat == 5)
+        hipLaunchKernelGGL(store_b32_kernel, dim3(r->grid), dim3(256), 0, s, r->out, r->n, r->obytes / 4u);
+    else if (r->flat == 4)
         hipLaunchKernelGGL(copy11_kernel, dim3(r->grid), dim3(256), 0, s, (const u32x4_t*)r->umem,
                            (uint64_t)r->n * r->stride / 16u, (u32x4_t*)r->out);
     else if (r->flat == 3)
@@ -264,6 +292,16 @@ int dqdk_gpu_membench_read(const void* d_buf, uint64_t bytes, void* stream, int 
 int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame_bytes, uint32_t n, void* d_out,
                              uint32_t out_bytes_per_frame, int flat, void* stream, int iters, double* ms_per_pass)
 {
+    if (flat == 5) {  // write calibration: no frames read (d_umem unused)
+        if (!d_out || !n || out_bytes_per_frame > 252 || (out_bytes_per_frame & 3) || ((uintptr_t)d_out & 255) ||
+            iters <= 0 || !ms_per_pass)
+            return -EINVAL;
+        FramesCtx c{nullptr, 0, 0, n, (uint32_t*)d_out, out_bytes_per_frame, cu_count() * 8u, 5, 0};
+        float ms = 0.f;
+        int rc = timed((hipStream_t)stream, iters, &ms, launch_frames, &c);
+        *ms_per_pass = (double)ms / iters;
+        return rc;
+    }
     if (!d_umem || !n || stride < frame_bytes || (stride & 15) || (frame_bytes & 15) || ((uintptr_t)d_umem & 15) ||
         ((uintptr_t)d_out & 15) || iters <= 0 || !ms_per_pass || (out_bytes_per_frame & 3))
         return -EINVAL;

@@ -268,7 +268,12 @@ int dqdk_gpu_membench_atomic(uint32_t* d_table, uint64_t entries, const uint32_t
  * as 0 with 16-B record stores (4 words per lane) instead of 4-B ones;
  * flat = 3: no frames, n * stride bytes read contiguously and a quarter of
  * that written (d_out must hold n * stride / 4 bytes); flat = 4: a plain
- * 1:1 copy of n * stride bytes into d_out. */
+ * 1:1 copy of n * stride bytes into d_out; flat = 5: write calibration, no
+ * frames (d_umem ignored): n wave instructions of 4-B-per-lane stores, each
+ * 64 aligned dwords (out_bytes_per_frame = 0) or a run of
+ * out_bytes_per_frame / 4 (< 64) dwords at an unaligned offset, runs of one
+ * wave adjacent (d_out 256-B aligned, sized by the caller for
+ * n * 256 + 64 K bytes). */
 int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame_bytes, uint32_t n, void* d_out,
                              uint32_t out_bytes_per_frame, int flat, void* stream, int iters, double* ms_per_pass);
 

@@ -51,7 +51,7 @@ def main():
     d = Path(sys.argv[1])
     out = summarise(d)
     for k, m in sorted(out.items()):
-        if not k.startswith("rx_"):
+        if k.startswith("__amd"):
             continue
         print(k)
         for c, v in sorted(m.items()):
