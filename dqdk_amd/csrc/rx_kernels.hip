@@ -387,6 +387,7 @@ constexpr int kLdsCnt = kLdsOob + kWaves * 64;
 struct DecodeLds {
     uint32_t cnt[kLdsCnt];       // [0, kL1Buckets): keys per L1 bucket (partitioned histogram)
     uint32_t sum[kWaves * 64];   // checksum word sums per frame
+    uint32_t sink[64];           // per-lane dump word (frame_sum_add)
     u32x4 tail[kWaves * 64];     // last checksum chunk per frame (tail correction)
 };
 
@@ -438,6 +439,29 @@ __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uin
 __device__ __forceinline__ void lds_add_u32(uint32_t lds_addr, uint32_t v)
 {
     asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+}
+
+// The frame's checksum word sum into its LDS slot.  One add from every lane
+// to one address serialises 64 LDS cycles (PMC: bank-conflict cycles were
+// 83 % of the fused decode's LDS cycles); instead the row sums are formed by
+// DPP and only the four row-end lanes add to the slot, the others to their
+// own sink word (distinct banks).
+#ifndef DQDK_SUM_DPP
+#define DQDK_SUM_DPP 1
+#endif
+__device__ __forceinline__ void frame_sum_add(uint32_t* slot, uint32_t* sink, uint32_t t, bool row_end)
+{
+#if DQDK_SUM_DPP
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x111, 0xf, 0xf, false);  // row_shr:1
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x112, 0xf, 0xf, false);  // row_shr:2
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x114, 0xf, 0xf, false);  // row_shr:4
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x118, 0xf, 0xf, false);  // row_shr:8
+    lds_add_u32((uint32_t)(uintptr_t)(row_end ? slot : sink), t);
+#else
+    (void)sink;
+    (void)row_end;
+    lds_add_u32((uint32_t)(uintptr_t)slot, t);
+#endif
 }
 
 // One event per 16-B chunk v (event byte 2 at byte r of v.x): key record
@@ -677,7 +701,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
                     // one address (inline asm: the compiler's atomic optimizer would turn
                     // a uniform-address atomicAdd into a 64-step readlane loop)
 #ifndef DQDK_DIAG_NOLDS
-                    lds_add_u32((uint32_t)(uintptr_t)&lds.sum[wslot0 + jp], acc0 + acc1);
+                    frame_sum_add(&lds.sum[wslot0 + jp], &lds.sink[lane], acc0 + acc1, (lane & 15) == 15);
 #endif
                     acc0 = acc1 = 0;
                     wp = 0;
@@ -816,6 +840,79 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
     __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, ooff, 0, 0);
 }
 
+// Both chunks of a window at once, without divergent branches: every lane
+// issues two returning LDS adds (an event's bucket stage count, a frame's
+// out-of-bounds count, or -- lanes without an event -- a private sink word of
+// the lane), one wait, then two stage stores (a slot past kFCap, or no event:
+// the lane's sink word).  The stage counts' latency is paid once per window
+// instead of once per chunk, and no exec mask is saved or restored.  Keys
+// past kFCap (rare) go to the block's overflow region behind one
+// wave-uniform branch.
+#ifndef DQDK_FPAIR
+#define DQDK_FPAIR 1
+#endif
+// Stage counts (and per-frame out-of-bounds counts) step by kCntUnit: with 4
+// a count is the byte offset of the slot, so a stage address is one mad.
+constexpr uint32_t kCntUnit = DQDK_FPAIR >= 2 ? 4u : 1u;
+__device__ __forceinline__ void fused_pair(const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0, uint32_t Ef,
+                                           uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc,
+                                           uint32_t lane)
+{
+    uint32_t key[2], b[2];
+    uint32_t* cnt[2];
+    bool ink[2];
+    // the lane's sink: the 64 slack words after the last bucket's stage (read
+    // by the flush of bucket 283 only past its count, so never stored)
+    uint32_t* const sink = &lds.stage[kL1Buckets * kFCap + lane];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const u32x4& v = c ? vb : va;
+        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
+        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
+        const uint32_t ch = x & 0xffffu;
+        const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);  // event bytes 5,6 = energy >> 8
+        const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);            // hist_class:3
+        key[c] = __umul24(ch, kHists << 16) + (hc << 16) + bin;        // ((ch*6 + hc) << 16) | bin
+        const bool inb = ch < kChannels && hc < kHists;                 // tristan.c:236-241
+        const bool has = e0 + 64u * c < Ef;
+        b[c] = min(key[c] >> kL1Shift, (uint32_t)kL1Buckets - 1);
+        ink[c] = has && inb;
+        cnt[c] = has ? (inb ? &lds.scnt[b[c]] : &lds.oob[oob_slot]) : sink;
+    }
+#if DQDK_FPAIR >= 2
+    // counts in bytes: the slot's stage address is b * (4 kFCap) + count
+    const uint32_t s0 = atomicAdd(cnt[0], kCntUnit);
+    const uint32_t s1 = atomicAdd(cnt[1], kCntUnit);
+    const bool st0 = ink[0] && s0 < 4u * kFCap, st1 = ink[1] && s1 < 4u * kFCap;
+    uint8_t* const stage8 = (uint8_t*)lds.stage;
+    *(uint32_t*)(st0 ? stage8 + __umul24(b[0], 4u * kFCap) + s0 : (uint8_t*)sink) = key[0];
+    *(uint32_t*)(st1 ? stage8 + __umul24(b[1], 4u * kFCap) + s1 : (uint8_t*)sink) = key[1];
+    const bool ov0 = ink[0] && s0 >= 4u * kFCap, ov1 = ink[1] && s1 >= 4u * kFCap;
+    if (__builtin_amdgcn_ballot_w64(ov0 || ov1)) {  // rare: overflow slots, one LDS atomic per wave
+        const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
+#else
+    const uint32_t s0 = atomicAdd(cnt[0], 1u);
+    const uint32_t s1 = atomicAdd(cnt[1], 1u);
+    const bool st0 = ink[0] && s0 < (uint32_t)kFCap, st1 = ink[1] && s1 < (uint32_t)kFCap;
+    *(st0 ? &lds.stage[b[0] * kFCap + s0] : sink) = key[0];
+    *(st1 ? &lds.stage[b[1] * kFCap + s1] : sink) = key[1];
+    const bool ov0 = ink[0] && s0 >= (uint32_t)kFCap, ov1 = ink[1] && s1 >= (uint32_t)kFCap;
+    const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
+    if (m0 | m1) {  // rare: overflow slots, one LDS atomic per wave
+#endif
+        const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
+        const uint32_t first = (uint32_t)__builtin_ctzll(m0 | m1);
+        uint32_t base = 0;
+        if (lane == first)
+            base = atomicAdd(&lds.ovf_n, n0 + (uint32_t)__builtin_popcountll(m1));
+        base = rdl(base, first);
+        const uint32_t r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+        const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+        __builtin_amdgcn_raw_buffer_store_b32(key[0], ovf_rsrc, ov0 ? 4u * (base + r0) : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(key[1], ovf_rsrc, ov1 ? 4u * (base + n0 + r1) : kOOB, 0, 0);
+    }
+}
+
 // Append the round's staged runs to the block's pieces.  Wave w owns buckets
 // w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece cursor `cur`).
 // All LDS reads of a few buckets are issued before their stores, and every
@@ -829,7 +926,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
     const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
     uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
-        c = min(lds.scnt[b], (uint32_t)kFCap);
+        c = min(lds.scnt[b] / kCntUnit, (uint32_t)kFCap);
         // lines mode: whole 128-B lines only (the piece cursor stays line-
         // aligned, so no store writes part of a line); the rest is carried
         w = kLines && !last ? (c & ~31u) : c;
@@ -894,7 +991,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
             lds.stage[bj * kFCap + lane] = x;
     }
     if (b < (uint32_t)kL1Buckets)
-        lds.scnt[b] = c - w;
+        lds.scnt[b] = (c - w) * kCntUnit;
 }
 
 // Two policies for the pieces' partial lines (runs end mid-line), chosen by
@@ -1001,14 +1098,21 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 } else {
                     csum_pair(b0[d], b1[d], u16x2{1, 1}, u16x2{1, 1}, acc0, acc1);
                 }
-                if (active && wp == P.tw && lane == (int)P.tl)
-                    lds.tail[wslot0 + jp] = P.th ? b1[d] : b0[d];
+                if (active && wp == P.tw) {  // (wave-uniform) the frame's last checksum chunk
+                    if (lane == (int)P.tl)
+                        lds.tail[wslot0 + jp] = P.th ? b1[d] : b0[d];
+                }
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
+#if DQDK_FPAIR
+                fused_pair(b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
+#else
                 fused_chunk(b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
                 fused_chunk(b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
+#endif
                 if (active && ++wp == P.nwin) {
-                    lds_add_u32((uint32_t)(uintptr_t)&lds.sum[wslot0 + jp], acc0 + acc1);
+                    frame_sum_add(&lds.sum[wslot0 + jp], &lds.stage[kL1Buckets * kFCap + lane], acc0 + acc1,
+                                  (lane & 15) == 15);
                     acc0 = acc1 = 0;
                     wp = 0;
                     pmask &= pmask - 1;
@@ -1032,7 +1136,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 
         // ---- phase C ----
         const uint32_t my = wslot0 + (uint32_t)lane;
-        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my];
+        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my] / kCntUnit;
         lds.sum[my] = 0;
         lds.oob[my] = 0;
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);

@@ -15,11 +15,14 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import dqdk_amd as D  # noqa: E402
 
 
-def rate(sync: bool, n: int, batches: int, mode: int) -> dict:
+def rate(sync: bool, n: int, batches: int, mode: int, sink: str = "file") -> dict:
     os.environ["DQDK_GPU_RAW_SYNC"] = "1" if sync else "0"
     cfg = D.RxConfig(payloadsz=1458, mode=mode, flags=D.F_CSUM)
     imgs = [D.synth_umem(n, 1500, 4096, queue=k, threads=16) for k in range(2)]
-    fd, path = tempfile.mkstemp(dir="/tmp")
+    if sink == "null":
+        fd, path = os.open("/dev/null", os.O_WRONLY), None
+    else:
+        fd, path = tempfile.mkstemp(dir="/tmp")
     try:
         with D.RxQueue(0, cfg, n) as q:
             for u, _ in imgs:
@@ -33,19 +36,31 @@ def rate(sync: bool, n: int, batches: int, mode: int) -> dict:
             q.sync()
             sec = time.perf_counter() - t0
             q.set_raw_fd(-1)
-        size = os.path.getsize(path)
+        size = os.path.getsize(path) if path else None
     finally:
         os.close(fd)
-        os.unlink(path)
-    assert size == (batches + 1) * n * 1458, size
+        if path:
+            os.unlink(path)
+    assert size in (None, (batches + 1) * n * 1458), size
     return {"Mpkt_s": round(n * batches / sec / 1e6, 3), "raw_GB_s": round(n * 1458 * batches / sec / 1e9, 3)}
 
 
 def main():
     n, batches = 1 << 16, 24
     out = {"frames_per_batch": n, "batches": batches, "frame_len": 1500}
+    # no raw fd: the host drop-in alone (zero-copy reads of the registered UMEM)
+    os.environ["DQDK_GPU_RAW_SYNC"] = "0"
+    imgs = [D.synth_umem(n, 1500, 4096, queue=k, threads=16) for k in range(2)]
+    with D.RxQueue(0, D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM), n) as q:
+        q.process_batch(*imgs[0])
+        t0 = time.perf_counter()
+        for b in range(batches):
+            q.process_batch(*imgs[b % 2])
+        out["no_raw_Mpkt_s"] = round(n * batches / (time.perf_counter() - t0) / 1e6, 3)
     for mode_name, mode in (("waveform", D.MODE_WAVEFORM), ("listmode", D.MODE_LISTMODE)):
-        out[mode_name] = {"serial": rate(True, n, batches, mode), "side_stream": rate(False, n, batches, mode)}
+        for sink in ("file", "null"):
+            out[f"{mode_name}_{sink}"] = {"serial": rate(True, n, batches, mode, sink),
+                                          "side_stream": rate(False, n, batches, mode, sink)}
     print(json.dumps(out), flush=True)
 
 
