@@ -77,6 +77,8 @@ def parse_args(argv=None):
     p.add_argument("--share-gpu", action="store_true",
                    help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
                         "collectives over gloo (the data path has none); the numbers are not a scaling result")
+    p.add_argument("--umem-alloc", choices=("torch", "contig"), default="torch",
+                   help="device UMEM image: torch caching allocator, or hipExtMallocWithFlags(contiguous)")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_summary.json"),
                    help="rocprofv3 PMC summary used for roofline.traffic")
     return p.parse_args(argv)
@@ -114,14 +116,51 @@ def spawn_ranks(n: int) -> int:
 
 # ---- one workload ----------------------------------------------------------------
 
-def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16):
+class DeviceImage:
+    """A device buffer from hipExtMallocWithFlags (hipDeviceMallocContiguous:
+    physically contiguous, so the image is mapped with large fragments
+    whatever the state of the device's memory), wrapped as a torch tensor."""
+
+    def __init__(self, torch, dev, size: int):
+        import ctypes as C
+        self.hip = C.CDLL("libamdhip64.so")
+        self.hip.hipExtMallocWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        self.hip.hipFree.argtypes = [C.c_void_p]
+        p = C.c_void_p()
+        rc = self.hip.hipExtMallocWithFlags(C.byref(p), size, 0x4)  # hipDeviceMallocContiguous
+        if rc != 0 or not p.value:
+            raise RuntimeError(f"hipExtMallocWithFlags(contiguous, {size}) failed: {rc}")
+        self.ptr, self.size = p.value, size
+        self.tensor = torch.as_tensor(_cuda_array(self.ptr, size, dev.index), device=dev)
+
+    def free(self):
+        if self.ptr:
+            self.hip.hipFree(self.ptr)
+            self.ptr = None
+
+
+def _cuda_array(ptr: int, size: int, device: int):
+    """__cuda_array_interface__ view of raw device memory (uint8)."""
+    class _A:
+        __cuda_array_interface__ = {"shape": (size,), "typestr": "|u1", "data": (ptr, False), "version": 3,
+                                    "strides": None}
+    return _A()
+
+
+def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="torch"):
     """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
-    (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample)."""
+    (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample,
+    owner of a contiguous image or None)."""
     import dqdk_amd._lib as LIB
     c = D.rx.synth_cfg(L, stride, queue)
     size = int(LIB.lib().dqdk_synth_umem_size(__import__("ctypes").byref(c), n))
     size = (size + 15) // 16 * 16
-    d_umem = torch.empty(size, dtype=torch.uint8, device=dev)
+    owner = None
+    if alloc == "contig":
+        owner = DeviceImage(torch, dev, size)
+        d_umem = owner.tensor
+    else:
+        d_umem = torch.empty(size, dtype=torch.uint8, device=dev)
     descs = []
     sample = None
     for f0 in range(0, n, chunk):
@@ -135,7 +174,7 @@ def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16):
             sample = (u, d.copy())  # the CPU baseline's sample: the workload's first frames
     desc = np.concatenate(descs)
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-    return d_umem, d_desc, desc, sample
+    return d_umem, d_desc, desc, sample, owner
 
 
 def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
@@ -160,7 +199,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
     pass_records = (args.records or not histo) and not args.no_records
 
     # ---- input: queue `rank` of the synthetic UMEM replay, resident in HBM ----
-    d_umem, d_desc, desc, sample = synth_to_device(D, torch, dev, n, L, stride, queue=rank)
+    d_umem, d_desc, desc, sample, owner = synth_to_device(D, torch, dev, n, L, stride, queue=rank,
+                                                          alloc=args.umem_alloc)
     umem_bytes = d_umem.numel()
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
@@ -332,7 +372,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                 "frames_per_launch": n,
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
-                "measured_frames_pattern_GB_s": pattern}
+                "measured_frames_pattern_GB_s": pattern,
+                "umem_image": {"alloc": args.umem_alloc, "va": hex(d_umem.data_ptr()),
+                               "va_mod_2MiB": d_umem.data_ptr() % (2 << 20), "bytes": umem_bytes}}
 
     # ---- CPU baseline: the oracle (C restatement), rank 0, outside the timed region ----
     cpu = None
@@ -343,6 +385,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
 
     q.close()
     del d_umem, d_desc, d_res, d_keys
+    if owner is not None:
+        torch.cuda.synchronize(dev)
+        owner.free()
     torch.cuda.empty_cache()
     return {
         "value": round(mpkts, 3), "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -106,13 +106,13 @@ def test_fused_peaked_faulty_overflows_pieces():
     of the events on four hot bins in three L1 buckets): the LDS stages of
     those buckets overflow every round and their per-block pieces fill, so
     keys go through the block overflow regions into rx_part1; bins receive
-    far more than 65535 events (rx_slice_heavy's u32 form).  Two batches:
+    far more than 65535 events.  Two batches:
     the second adds onto the first in the table."""
     n = 1 << 20
     umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, peaked=True, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
     res, cnt, table, launches = run_bench_form(umem, desc, cfg, batches=2)
-    assert launches.get("rx_fixup", 0) == 2 and launches.get("rx_slice_heavy", 0) >= 1, launches
+    assert launches.get("rx_fixup", 0) == 2 and launches.get("rx_slice_histo", 0) >= 1, launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     otable *= 2
     ocnt = {k: (v if k == "first_abort_idx" else 2 * v) for k, v in ocnt.items()}
