@@ -77,8 +77,8 @@ def parse_args(argv=None):
     p.add_argument("--share-gpu", action="store_true",
                    help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
                         "collectives over gloo (the data path has none); the numbers are not a scaling result")
-    p.add_argument("--umem-alloc", choices=("torch", "contig"), default="torch",
-                   help="device UMEM image: torch caching allocator, or hipExtMallocWithFlags(contiguous)")
+    p.add_argument("--umem-alloc", choices=("torch", "contig"), default="contig",
+                   help="device UMEM image: dqdk_gpu_device_alloc (contiguous, default) or torch's allocator")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_summary.json"),
                    help="rocprofv3 PMC summary used for roofline.traffic")
     return p.parse_args(argv)
@@ -116,37 +116,6 @@ def spawn_ranks(n: int) -> int:
 
 # ---- one workload ----------------------------------------------------------------
 
-class DeviceImage:
-    """A device buffer from hipExtMallocWithFlags (hipDeviceMallocContiguous:
-    physically contiguous, so the image is mapped with large fragments
-    whatever the state of the device's memory), wrapped as a torch tensor."""
-
-    def __init__(self, torch, dev, size: int):
-        import ctypes as C
-        self.hip = C.CDLL("libamdhip64.so")
-        self.hip.hipExtMallocWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
-        self.hip.hipFree.argtypes = [C.c_void_p]
-        p = C.c_void_p()
-        rc = self.hip.hipExtMallocWithFlags(C.byref(p), size, 0x4)  # hipDeviceMallocContiguous
-        if rc != 0 or not p.value:
-            raise RuntimeError(f"hipExtMallocWithFlags(contiguous, {size}) failed: {rc}")
-        self.ptr, self.size = p.value, size
-        self.tensor = torch.as_tensor(_cuda_array(self.ptr, size, dev.index), device=dev)
-
-    def free(self):
-        if self.ptr:
-            self.hip.hipFree(self.ptr)
-            self.ptr = None
-
-
-def _cuda_array(ptr: int, size: int, device: int):
-    """__cuda_array_interface__ view of raw device memory (uint8)."""
-    class _A:
-        __cuda_array_interface__ = {"shape": (size,), "typestr": "|u1", "data": (ptr, False), "version": 3,
-                                    "strides": None}
-    return _A()
-
-
 def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="torch"):
     """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
     (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample,
@@ -156,8 +125,8 @@ def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="to
     size = int(LIB.lib().dqdk_synth_umem_size(__import__("ctypes").byref(c), n))
     size = (size + 15) // 16 * 16
     owner = None
-    if alloc == "contig":
-        owner = DeviceImage(torch, dev, size)
+    if alloc == "contig":  # the library's device allocation (physically contiguous where possible)
+        owner = D.DeviceBuffer(dev.index, size)
         d_umem = owner.tensor
     else:
         d_umem = torch.empty(size, dtype=torch.uint8, device=dev)
@@ -387,7 +356,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
     del d_umem, d_desc, d_res, d_keys
     if owner is not None:
         torch.cuda.synchronize(dev)
-        owner.free()
+        owner.close()
     torch.cuda.empty_cache()
     return {
         "value": round(mpkts, 3), "ms_per_step": round(elapsed / args.steps * 1e3, 4),

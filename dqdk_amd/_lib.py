@@ -104,6 +104,8 @@ SIGNATURES = {
                                            C.c_char_p, C.c_char_p, C.c_uint64]),
     "dqdk_gpu_membench_read": (C.c_int, [_P, C.c_uint64, _P, C.c_int, C.POINTER(C.c_double)]),
     "dqdk_gpu_membench_atomic": (C.c_int, [_P, C.c_uint64, _P, C.c_uint64, _P, C.c_int, C.POINTER(C.c_double)]),
+    "dqdk_gpu_device_alloc": (C.c_int, [C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "dqdk_gpu_device_free": (C.c_int, [C.c_int, _P]),
     "dqdk_gpu_membench_frames": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, _P, C.c_uint32, C.c_int, _P,
                                            C.c_int, C.POINTER(C.c_double)]),
     "dqdk_gpu_timing_enable": (C.c_int, [_P, C.c_int]),

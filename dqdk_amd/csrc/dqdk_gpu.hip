@@ -97,6 +97,39 @@ struct Reg {
     void* dev;
 };
 
+// Large device buffers (the table, the staging regions) are allocated
+// physically contiguous (hipDeviceMallocContiguous) when the device allows:
+// the kernels walk them at strides and in gathers whose address translation
+// then stays within large fragments (measured on the UMEM image, which the
+// caller allocates: 9000 B decode 2.27 ms from a contiguous image, 2.45 ms
+// from a hipMalloc'd one, every run).  DQDK_GPU_CONTIG=0 turns it
+// off; an allocation the driver refuses contiguous falls back to hipMalloc.
+int g_contig = -1;
+
+bool contig_enabled()
+{
+    if (g_contig < 0) {
+        const char* e = getenv("DQDK_GPU_CONTIG");
+        g_contig = e ? (atoi(e) != 0) : 1;
+    }
+    return g_contig != 0;
+}
+
+template <typename T>
+hipError_t dev_alloc(T** p, size_t bytes)
+{
+    void* v = nullptr;
+    hipError_t e = hipErrorOutOfMemory;
+    if (contig_enabled() && bytes >= (1u << 21))
+        e = hipExtMallocWithFlags(&v, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // a refused contiguous request is not an error of the queue
+        e = hipMalloc(&v, bytes);
+    }
+    *p = (T*)v;
+    return e;
+}
+
 }  // namespace
 
 struct dqdk_gpu_queue {
@@ -658,8 +691,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));
     if (q->histo) {
-        if ((e = hipMalloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMalloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
+        if ((e = dev_alloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
+            (e = dev_alloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
             return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
         if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMemset(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
@@ -690,22 +723,49 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             const size_t pe = (size_t)part_elems(nk, q->fused_elems);
             q->part2_stride = (pe + 7) & ~(size_t)7;
             q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
-            if ((e = hipMalloc(&q->d_keys, nk * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part1, pe * 4)) != hipSuccess ||
-                (e = hipMalloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
-                (e = hipMalloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t))) != hipSuccess ||
-                (e = hipMalloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t))) != hipSuccess ||
+            if ((e = dev_alloc(&q->d_keys, nk * 4)) != hipSuccess ||
+                (e = dev_alloc(&q->d_part1, pe * 4)) != hipSuccess ||
+                (e = dev_alloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
+                (e = dev_alloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t))) != hipSuccess ||
+                (e = dev_alloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t))) != hipSuccess ||
                 (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
             // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
             const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
             const uint64_t grid = fg.grid;
             q->ovf_blk_elems = grid * ((nsuper + grid - 1) / grid) * (64 * kFWaves) * q->E;
-            if ((e = hipMalloc(&q->d_ovf_blk, q->ovf_blk_elems * 4)) != hipSuccess)
+            if ((e = dev_alloc(&q->d_ovf_blk, q->ovf_blk_elems * 4)) != hipSuccess)
                 return cleanup((fail("hipMalloc(overflow regions)", e), -ENOMEM));
         }
     }
     *out = q;
+    return 0;
+}
+
+int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out)
+{
+    if (!d_out || !size)
+        return fail_errno(-EINVAL, "device_alloc: bad argument");
+    *d_out = nullptr;
+    if (device < 0 || device >= dqdk_gpu_device_count())
+        return fail_errno(-ENODEV, "device_alloc: no such HIP device");
+    SETDEV(device);
+    void* p = nullptr;
+    hipError_t e = dev_alloc(&p, size);
+    if (e != hipSuccess)
+        return (fail("device_alloc", e), -ENOMEM);
+    *d_out = p;
+    return 0;
+}
+
+int dqdk_gpu_device_free(int device, void* d_ptr)
+{
+    if (!d_ptr)
+        return 0;
+    if (device < 0 || device >= dqdk_gpu_device_count())
+        return fail_errno(-ENODEV, "device_free: no such HIP device");
+    SETDEV(device);
+    HIPCHK(hipFree(d_ptr));
     return 0;
 }
 
@@ -1004,7 +1064,7 @@ uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q)
     DevGuard dev_guard_(q->device);
     if (dev_guard_.e != hipSuccess)
         return nullptr;
-    if (!q->d_snap && hipMalloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t)) != hipSuccess) {
+    if (!q->d_snap && dev_alloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t)) != hipSuccess) {
         q->d_snap = nullptr;
         return nullptr;
     }

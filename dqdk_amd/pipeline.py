@@ -71,9 +71,11 @@ class E2EPipeline:
         self.s_h2d, self.s_rx, self.s_d2h = (torch.cuda.Stream(self.dev) for _ in range(3))
         self.q.set_stream(self.s_rx.cuda_stream)
         self.slots = []
+        self.bufs = []  # the slots' UMEM images: library device allocations (contiguous where possible)
         for _ in range(depth):
+            self.bufs.append(R.DeviceBuffer(device, self.umem_bytes))
             self.slots.append({
-                "umem": torch.empty(self.umem_bytes, dtype=torch.uint8, device=self.dev),
+                "umem": self.bufs[-1].tensor,
                 "desc": torch.empty(n * 16, dtype=torch.uint8, device=self.dev),
                 "res": torch.empty(n * 8, dtype=torch.uint8, device=self.dev),
                 "keys": torch.empty(max(n * E, 1), dtype=torch.int32, device=self.dev) if records else None,
@@ -166,3 +168,8 @@ class E2EPipeline:
 
     def close(self):
         self.q.close()
+        torch.cuda.synchronize(self.dev)
+        for sl in self.slots:
+            sl["umem"] = None
+        for b in self.bufs:
+            b.close()

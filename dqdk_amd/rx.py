@@ -243,6 +243,40 @@ def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, d
     return buf.value.decode()
 
 
+class DeviceBuffer:
+    """HBM from dqdk_gpu_device_alloc (physically contiguous where the driver
+    allows): a device UMEM image or frame staging slot.  ``tensor`` is a torch
+    uint8 view of it (torch imported lazily; the buffer outlives the view only
+    until close())."""
+
+    def __init__(self, device: int, size: int):
+        p = C.c_void_p()
+        L.check(L.lib().dqdk_gpu_device_alloc(device, size, C.byref(p)), "device_alloc")
+        self.device, self.size, self.ptr = device, size, int(p.value)
+
+    @property
+    def tensor(self):
+        import torch
+
+        ptr, size = self.ptr, self.size
+
+        class _View:  # __cuda_array_interface__ of the raw allocation
+            __cuda_array_interface__ = {"shape": (size,), "typestr": "|u1", "data": (ptr, False), "version": 3,
+                                        "strides": None}
+        return torch.as_tensor(_View(), device=torch.device("cuda", self.device))
+
+    def close(self) -> None:
+        if self.ptr:
+            L.lib().dqdk_gpu_device_free(self.device, self.ptr)
+            self.ptr = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 # ---- synthetic UMEM (bench / test input) ------------------------------------
 
 SEED = 20261015  # SURVEY.md §8(d)
