@@ -116,16 +116,27 @@ def spawn_ranks(n: int) -> int:
 
 # ---- one workload ----------------------------------------------------------------
 
-def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="torch"):
-    """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
-    (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample,
-    owner of a contiguous image or None)."""
+def umem_size(D, n, L, stride, queue=0):
+    import ctypes
+
     import dqdk_amd._lib as LIB
     c = D.rx.synth_cfg(L, stride, queue)
-    size = int(LIB.lib().dqdk_synth_umem_size(__import__("ctypes").byref(c), n))
-    size = (size + 15) // 16 * 16
+    return (int(LIB.lib().dqdk_synth_umem_size(ctypes.byref(c), n)) + 15) // 16 * 16
+
+
+def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="torch", image=None):
+    """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
+    (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample,
+    owner of a library-allocated image or None).  `image`: a DeviceBuffer
+    allocated beforehand (main() allocates the images first, while the
+    device's memory is unfragmented)."""
+    size = umem_size(D, n, L, stride, queue)
     owner = None
-    if alloc == "contig":  # the library's device allocation (physically contiguous where possible)
+    if image is not None:
+        assert image.size >= size
+        owner = image
+        d_umem = image.tensor[:size]
+    elif alloc == "contig":  # the library's device allocation (physically contiguous where possible)
         owner = D.DeviceBuffer(dev.index, size)
         d_umem = owner.tensor
     else:
@@ -146,7 +157,7 @@ def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="to
     return d_umem, d_desc, desc, sample, owner
 
 
-def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
+def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     import ctypes as C
 
     import dqdk_amd as D
@@ -169,7 +180,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
 
     # ---- input: queue `rank` of the synthetic UMEM replay, resident in HBM ----
     d_umem, d_desc, desc, sample, owner = synth_to_device(D, torch, dev, n, L, stride, queue=rank,
-                                                          alloc=args.umem_alloc)
+                                                          alloc=args.umem_alloc, image=image)
     umem_bytes = d_umem.numel()
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
@@ -342,7 +353,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
                 "measured_frames_pattern_GB_s": pattern,
-                "umem_image": {"alloc": args.umem_alloc, "va": hex(d_umem.data_ptr()),
+                "umem_image": {"alloc": args.umem_alloc,
+                               "contiguous": bool(owner.contiguous) if owner is not None else False,
+                               "va": hex(d_umem.data_ptr()),
                                "va_mod_2MiB": d_umem.data_ptr() % (2 << 20), "bytes": umem_bytes}}
 
     # ---- CPU baseline: the oracle (C restatement), rank 0, outside the timed region ----
@@ -354,7 +367,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec):
 
     q.close()
     del d_umem, d_desc, d_res, d_keys
-    if owner is not None:
+    if owner is not None and image is None:
         torch.cuda.synchronize(dev)
         owner.close()
     torch.cuda.empty_cache()
@@ -540,18 +553,31 @@ def main():
 
     cpu_sec = 0.0 if args.no_cpu_baseline else args.cpu_baseline_sec
     extra = {}
+    images = {}
     if args.cpu_dry_run:
         r = dry_run(args, torch, dist, dev, rank, world)
     elif args.e2e:
         r = run_e2e(args, torch, dist, dev, rank, world, local)
     else:
-        r = measure(args, args.frame_len, torch, dist, dev, rank, world, local, cpu_sec)
-        if args.frame_len == 1500 and not args.no_9000 and not args.stride and not args.payloadsz:
-            r9 = measure(args, 9000, torch, dist, dev, rank, world, local, cpu_sec / 2)
+        both = args.frame_len == 1500 and not args.no_9000 and not args.stride and not args.payloadsz
+        if args.umem_alloc == "contig":
+            # the UMEM images first, while the device's memory is unfragmented
+            # (a contiguous image is what keeps the decode's address
+            # translation in large fragments: DESIGN.md)
+            import dqdk_amd as D
+            for L in ([args.frame_len, 9000] if both else [args.frame_len]):
+                stride = args.stride or (4096 if 0 < L <= 4096 else 9216)
+                images[L] = D.DeviceBuffer(dev.index, umem_size(D, args.frames, L, stride, rank))
+        r = measure(args, args.frame_len, torch, dist, dev, rank, world, local, cpu_sec, images.get(args.frame_len))
+        if both:
+            r9 = measure(args, 9000, torch, dist, dev, rank, world, local, cpu_sec / 2, images.get(9000))
             extra = {"by_frame_len": {"1500": {"value": r["value"], "frame_GB_s": r["frame_GB_s"],
                                                "ms_per_step": r["ms_per_step"]},
                                       "9000": r9}}
 
+    for im in images.values():
+        torch.cuda.synchronize(dev)
+        im.close()
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -97,31 +97,35 @@ struct Reg {
     void* dev;
 };
 
-// Large device buffers (the table, the staging regions) are allocated
-// physically contiguous (hipDeviceMallocContiguous) when the device allows:
-// the kernels walk them at strides and in gathers whose address translation
-// then stays within large fragments (measured on the UMEM image, which the
-// caller allocates: 9000 B decode 2.27 ms from a contiguous image, 2.45 ms
-// from a hipMalloc'd one, every run).  DQDK_GPU_CONTIG=0 turns it
-// off; an allocation the driver refuses contiguous falls back to hipMalloc.
+// Device memory, plain (hipMalloc) or physically contiguous
+// (hipDeviceMallocContiguous).  The UMEM image a caller allocates through
+// dqdk_gpu_device_alloc is contiguous: the decode walks the frames at their
+// UMEM stride, and from a contiguous image its address translation stays
+// within large fragments (9000 B: 2.27-2.30 ms per 1M-frame batch against
+// 2.45 ms from a hipMalloc'd image, every run).  The queue's own
+// table and staging stay plain: contiguous, the fused decode's piece stores
+// and rx_hist_prep ran slower (1500 B decode 0.462 -> 0.482 ms, prep 0.012 ->
+// 0.028 ms, same box); DQDK_GPU_CONTIG=1 allocates them contiguous too.
 int g_contig = -1;
 
-bool contig_enabled()
+bool contig_internal()
 {
     if (g_contig < 0) {
         const char* e = getenv("DQDK_GPU_CONTIG");
-        g_contig = e ? (atoi(e) != 0) : 1;
+        g_contig = e ? (atoi(e) != 0) : 0;
     }
     return g_contig != 0;
 }
 
 template <typename T>
-hipError_t dev_alloc(T** p, size_t bytes)
+hipError_t dev_alloc(T** p, size_t bytes, bool contig = contig_internal(), bool* got_contig = nullptr)
 {
     void* v = nullptr;
     hipError_t e = hipErrorOutOfMemory;
-    if (contig_enabled() && bytes >= (1u << 21))
+    if (contig && bytes >= (1u << 21))
         e = hipExtMallocWithFlags(&v, bytes, hipDeviceMallocContiguous);
+    if (got_contig)
+        *got_contig = e == hipSuccess;
     if (e != hipSuccess) {
         (void)hipGetLastError();  // a refused contiguous request is not an error of the queue
         e = hipMalloc(&v, bytes);
@@ -751,11 +755,12 @@ int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out)
         return fail_errno(-ENODEV, "device_alloc: no such HIP device");
     SETDEV(device);
     void* p = nullptr;
-    hipError_t e = dev_alloc(&p, size);
+    bool contig = false;
+    hipError_t e = dev_alloc(&p, size, true, &contig);
     if (e != hipSuccess)
         return (fail("device_alloc", e), -ENOMEM);
     *d_out = p;
-    return 0;
+    return contig ? 0 : 1;
 }
 
 int dqdk_gpu_device_free(int device, void* d_ptr)

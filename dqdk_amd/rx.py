@@ -251,8 +251,10 @@ class DeviceBuffer:
 
     def __init__(self, device: int, size: int):
         p = C.c_void_p()
-        L.check(L.lib().dqdk_gpu_device_alloc(device, size, C.byref(p)), "device_alloc")
+        rc = L.lib().dqdk_gpu_device_alloc(device, size, C.byref(p))
+        L.check(min(rc, 0), "device_alloc")
         self.device, self.size, self.ptr = device, size, int(p.value)
+        self.contiguous = rc == 0
 
     @property
     def tensor(self):
