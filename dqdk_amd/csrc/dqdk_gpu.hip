@@ -97,39 +97,127 @@ struct Reg {
     void* dev;
 };
 
-// Device memory, plain (hipMalloc) or physically contiguous
-// (hipDeviceMallocContiguous).  The UMEM image a caller allocates through
-// dqdk_gpu_device_alloc is contiguous: the decode walks the frames at their
-// UMEM stride, and from a contiguous image its address translation stays
-// within large fragments (9000 B: 2.27-2.30 ms per 1M-frame batch against
-// 2.45 ms from a hipMalloc'd image, every run).  The queue's own
-// table and staging stay plain: contiguous, the fused decode's piece stores
-// and rx_hist_prep ran slower (1500 B decode 0.462 -> 0.482 ms, prep 0.012 ->
-// 0.028 ms, same box); DQDK_GPU_CONTIG=1 allocates them contiguous too.
-int g_contig = -1;
+// Device memory: plain (hipMalloc), physically contiguous
+// (hipDeviceMallocContiguous), or VMM (hipMemCreate physical chunks of the
+// recommended granularity mapped at a reserved range).  Chosen by
+// DQDK_GPU_ALLOC (the queue's table and staging) and DQDK_GPU_IMAGE_ALLOC
+// (dqdk_gpu_device_alloc: UMEM images) = plain | contig | vmm; what is
+// measured and why the defaults are what they are: DESIGN.md.
+enum AllocKind { kAllocPlain = 0, kAllocContig = 1, kAllocVmm = 2 };
 
-bool contig_internal()
+int alloc_kind(const char* var, int dflt)
 {
-    if (g_contig < 0) {
-        const char* e = getenv("DQDK_GPU_CONTIG");
-        g_contig = e ? (atoi(e) != 0) : 0;
+    const char* e = getenv(var);
+    if (!e)
+        return dflt;
+    if (!strcmp(e, "contig"))
+        return kAllocContig;
+    if (!strcmp(e, "vmm"))
+        return kAllocVmm;
+    return kAllocPlain;
+}
+
+int internal_alloc_kind()
+{
+    static const int k = alloc_kind("DQDK_GPU_ALLOC", kAllocPlain);
+    return k;
+}
+
+int image_alloc_kind()
+{
+    static const int k = alloc_kind("DQDK_GPU_IMAGE_ALLOC", kAllocContig);
+    return k;
+}
+
+struct VmmRange {
+    void* va;
+    size_t size;
+    hipMemGenericAllocationHandle_t h;
+};
+std::mutex g_vmm_mu;
+std::vector<VmmRange> g_vmm;
+
+hipError_t vmm_alloc(void** p, size_t bytes)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    if (e == hipSuccess)
+        e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e != hipSuccess)
+        return e;
+    if (gran < (2u << 20))
+        gran = 2u << 20;
+    const size_t size = (bytes + gran - 1) / gran * gran;
+    hipMemGenericAllocationHandle_t h{};
+    void* va = nullptr;
+    if ((e = hipMemCreate(&h, size, &prop, 0)) != hipSuccess)
+        return e;
+    if ((e = hipMemAddressReserve(&va, size, gran, nullptr, 0)) != hipSuccess) {
+        (void)hipMemRelease(h);
+        return e;
     }
-    return g_contig != 0;
+    hipMemAccessDesc ad{};
+    ad.location = prop.location;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    if ((e = hipMemMap(va, size, 0, h, 0)) != hipSuccess || (e = hipMemSetAccess(va, size, &ad, 1)) != hipSuccess) {
+        (void)hipMemUnmap(va, size);
+        (void)hipMemAddressFree(va, size);
+        (void)hipMemRelease(h);
+        return e;
+    }
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    g_vmm.push_back({va, size, h});
+    *p = va;
+    return hipSuccess;
+}
+
+// frees what dev_alloc returned, whichever kind it was
+void dev_free(void* p)
+{
+    if (!p)
+        return;
+    {
+        std::lock_guard<std::mutex> g(g_vmm_mu);
+        for (size_t k = 0; k < g_vmm.size(); k++) {
+            if (g_vmm[k].va == p) {
+                const VmmRange r = g_vmm[k];
+                g_vmm.erase(g_vmm.begin() + (long)k);
+                (void)hipDeviceSynchronize();
+                (void)hipMemUnmap(r.va, r.size);
+                (void)hipMemAddressFree(r.va, r.size);
+                (void)hipMemRelease(r.h);
+                return;
+            }
+        }
+    }
+    (void)hipFree(p);
 }
 
 template <typename T>
-hipError_t dev_alloc(T** p, size_t bytes, bool contig = contig_internal(), bool* got_contig = nullptr)
+hipError_t dev_alloc(T** p, size_t bytes, int kind = internal_alloc_kind(), int* got = nullptr)
 {
     void* v = nullptr;
     hipError_t e = hipErrorOutOfMemory;
-    if (contig && bytes >= (1u << 21))
+    int k = kAllocPlain;
+    if (kind == kAllocContig && bytes >= (1u << 21)) {
         e = hipExtMallocWithFlags(&v, bytes, hipDeviceMallocContiguous);
-    if (got_contig)
-        *got_contig = e == hipSuccess;
-    if (e != hipSuccess) {
-        (void)hipGetLastError();  // a refused contiguous request is not an error of the queue
-        e = hipMalloc(&v, bytes);
+        k = kAllocContig;
+    } else if (kind == kAllocVmm && bytes >= (1u << 21)) {
+        e = vmm_alloc(&v, bytes);
+        k = kAllocVmm;
     }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // a refused request of the chosen kind falls back to hipMalloc
+        e = hipMalloc(&v, bytes);
+        k = kAllocPlain;
+    }
+    if (got)
+        *got = k;
     *p = (T*)v;
     return e;
 }
@@ -755,12 +843,13 @@ int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out)
         return fail_errno(-ENODEV, "device_alloc: no such HIP device");
     SETDEV(device);
     void* p = nullptr;
-    bool contig = false;
-    hipError_t e = dev_alloc(&p, size, true, &contig);
+    const int want = image_alloc_kind();
+    int got = kAllocPlain;
+    hipError_t e = dev_alloc(&p, size, want, &got);
     if (e != hipSuccess)
         return (fail("device_alloc", e), -ENOMEM);
     *d_out = p;
-    return contig ? 0 : 1;
+    return got == want ? 0 : 1;
 }
 
 int dqdk_gpu_device_free(int device, void* d_ptr)
@@ -770,7 +859,7 @@ int dqdk_gpu_device_free(int device, void* d_ptr)
     if (device < 0 || device >= dqdk_gpu_device_count())
         return fail_errno(-ENODEV, "device_free: no such HIP device");
     SETDEV(device);
-    HIPCHK(hipFree(d_ptr));
+    dev_free(d_ptr);
     return 0;
 }
 
@@ -791,18 +880,18 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     }
     for (auto ev : q->ev_free)
         (void)hipEventDestroy(ev);
-    (void)hipFree(q->d_hist);
-    (void)hipFree(q->d_lo);
-    (void)hipFree(q->d_snap);
+    dev_free(q->d_hist);
+    dev_free(q->d_lo);
+    dev_free(q->d_snap);
     (void)hipFree(q->d_cum);
     (void)hipFree(q->d_batch);
-    (void)hipFree(q->d_keys);
-    (void)hipFree(q->d_part1);
-    (void)hipFree(q->d_part2);
-    (void)hipFree(q->d_runs);
-    (void)hipFree(q->d_hscratch);
+    dev_free(q->d_keys);
+    dev_free(q->d_part1);
+    dev_free(q->d_part2);
+    dev_free(q->d_runs);
+    dev_free(q->d_hscratch);
     (void)hipFree(q->d_fix);
-    (void)hipFree(q->d_ovf_blk);
+    dev_free(q->d_ovf_blk);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     (void)hipFree(q->d_raw_blk);

@@ -1639,7 +1639,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
     __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1];
-    __shared__ uint32_t prow[2][kMaxFusedGrid + 64];  // (+64: the LDS-DMA fills whole 64-word wave rows)
+    __shared__ uint32_t prow[2][kMaxFusedGrid + 1];
     const int tid = threadIdx.x;
     const uint32_t nitems = a.scratch[kOffIstart + kL1Buckets];
     const uint32_t* items = a.scratch + kOffItems;
@@ -1721,38 +1721,18 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wq0 * 16u + lane) * 4u, j * 256, kLdAux);
         }
     };
-    // Pipeline (kP2Pipe): item i's keys are loaded during item i - grid; at
-    // the top of item i the geometry (item table entries) of items i + grid
-    // and i + 2 grid is fetched, and item i + 2 grid's piece row goes to LDS by
-    // DMA during the count, so no dependent global load sits between the
-    // barriers before item i + grid's key loads.
     uint32_t nk_next = 0;
     uint64_t base_next = 0;
     int pb = 0;
-    const uint32_t grid = gridDim.x;
     if (kP2Pipe && blockIdx.x < nitems) {
         geo(blockIdx.x, nk_next, base_next);
         stage_pieces(base_next, 0);
-        if (blockIdx.x + grid < nitems) {
-            uint32_t nk1;
-            uint64_t base1;
-            geo(blockIdx.x + grid, nk1, base1);
-            stage_pieces(base1, 1);
-        }
         P2_BARRIER();
         load(base_next, nk_next, 0);
     }
-    for (uint32_t item = blockIdx.x; item < nitems; item += grid, pb ^= 1) {
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
         uint32_t nk = nk_next;
         uint64_t base = base_next;
-        const bool more = kP2Pipe && item + grid < nitems;
-        const bool more2 = kP2Pipe && item + 2 * grid < nitems;
-        if (more)  // its piece row is in prow[pb ^ 1]
-            geo(item + grid, nk_next, base_next);
-        uint32_t nk2 = 0;
-        uint64_t base2 = 0;
-        if (more2)
-            geo(item + 2 * grid, nk2, base2);
         if (!kP2Pipe)
             geo(item, nk, base);
         if (tid < kSubs)
@@ -1776,15 +1756,6 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
             rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
         }
-        // (item + 2 grid)'s piece row straight into prow[pb] (free: this item's
-        // keys were loaded last iteration) by LDS-DMA, no register held: it
-        // lands while this item is scanned and scattered, and is complete
-        // before its use (each issuing wave's next key wait is younger)
-        if (more2 && gathered(base2) && (uint32_t)(tid & ~63) <= a.fgrid) {
-            const uint32_t* src = a.scratch + kOffPiecePre + ((uint32_t)base2 / (uint32_t)a.region) * (kMaxFusedGrid + 1);
-            __builtin_amdgcn_global_load_lds(src + min((uint32_t)tid, (uint32_t)kMaxFusedGrid),
-                                             (__attribute__((address_space(3))) void*)&prow[pb][tid & ~63], 4, 0, 0);
-        }
         P2_BARRIER();
         wave0_excl_scan(lcnt, loff, kSubs, false);
         P2_BARRIER();
@@ -1796,6 +1767,11 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
                     (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
         // the next item's keys load while this one is written out
+        const bool more = kP2Pipe && item + gridDim.x < nitems;
+        if (more) {
+            geo(item + gridDim.x, nk_next, base_next);
+            stage_pieces(base_next, pb ^ 1);
+        }
         P2_BARRIER();
         if (more)
             load(base_next, nk_next, pb ^ 1);
