@@ -97,13 +97,14 @@ struct Reg {
     void* dev;
 };
 
-// Device memory: plain (hipMalloc), physically contiguous
-// (hipDeviceMallocContiguous), or VMM (hipMemCreate physical chunks of the
-// recommended granularity mapped at a reserved range).  Chosen by
-// DQDK_GPU_ALLOC (the queue's table and staging) and DQDK_GPU_IMAGE_ALLOC
-// (dqdk_gpu_device_alloc: UMEM images) = plain | contig | vmm; what is
-// measured and why the defaults are what they are: DESIGN.md.
-enum AllocKind { kAllocPlain = 0, kAllocContig = 1, kAllocVmm = 2 };
+// Device memory: plain (hipMalloc) or physically contiguous
+// (hipDeviceMallocContiguous).  UMEM images from dqdk_gpu_device_alloc are
+// contiguous (DQDK_GPU_IMAGE_ALLOC=plain: plain); the queue's table and
+// staging follow DQDK_GPU_ALLOC = plain | contig | auto (default auto:
+// contiguous from 128 events per frame, where the fused decode flushes whole
+// lines; plain below, where contiguous staging made the decode slower).
+// Measurements: DESIGN.md.
+enum AllocKind { kAllocPlain = 0, kAllocContig = 1, kAllocAuto = 2 };
 
 int alloc_kind(const char* var, int dflt)
 {
@@ -112,94 +113,25 @@ int alloc_kind(const char* var, int dflt)
         return dflt;
     if (!strcmp(e, "contig"))
         return kAllocContig;
-    if (!strcmp(e, "vmm"))
-        return kAllocVmm;
+    if (!strcmp(e, "auto"))
+        return kAllocAuto;
     return kAllocPlain;
 }
 
-int internal_alloc_kind()
+int internal_alloc_kind(uint32_t E)
 {
-    static const int k = alloc_kind("DQDK_GPU_ALLOC", kAllocPlain);
-    return k;
+    static const int k = alloc_kind("DQDK_GPU_ALLOC", kAllocAuto);
+    return k == kAllocAuto ? (E >= 128 ? kAllocContig : kAllocPlain) : k;
 }
 
 int image_alloc_kind()
 {
     static const int k = alloc_kind("DQDK_GPU_IMAGE_ALLOC", kAllocContig);
-    return k;
-}
-
-struct VmmRange {
-    void* va;
-    size_t size;
-    hipMemGenericAllocationHandle_t h;
-};
-std::mutex g_vmm_mu;
-std::vector<VmmRange> g_vmm;
-
-hipError_t vmm_alloc(void** p, size_t bytes)
-{
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = dev;
-    size_t gran = 0;
-    if (e == hipSuccess)
-        e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
-    if (e != hipSuccess)
-        return e;
-    if (gran < (2u << 20))
-        gran = 2u << 20;
-    const size_t size = (bytes + gran - 1) / gran * gran;
-    hipMemGenericAllocationHandle_t h{};
-    void* va = nullptr;
-    if ((e = hipMemCreate(&h, size, &prop, 0)) != hipSuccess)
-        return e;
-    if ((e = hipMemAddressReserve(&va, size, gran, nullptr, 0)) != hipSuccess) {
-        (void)hipMemRelease(h);
-        return e;
-    }
-    hipMemAccessDesc ad{};
-    ad.location = prop.location;
-    ad.flags = hipMemAccessFlagsProtReadWrite;
-    if ((e = hipMemMap(va, size, 0, h, 0)) != hipSuccess || (e = hipMemSetAccess(va, size, &ad, 1)) != hipSuccess) {
-        (void)hipMemUnmap(va, size);
-        (void)hipMemAddressFree(va, size);
-        (void)hipMemRelease(h);
-        return e;
-    }
-    std::lock_guard<std::mutex> g(g_vmm_mu);
-    g_vmm.push_back({va, size, h});
-    *p = va;
-    return hipSuccess;
-}
-
-// frees what dev_alloc returned, whichever kind it was
-void dev_free(void* p)
-{
-    if (!p)
-        return;
-    {
-        std::lock_guard<std::mutex> g(g_vmm_mu);
-        for (size_t k = 0; k < g_vmm.size(); k++) {
-            if (g_vmm[k].va == p) {
-                const VmmRange r = g_vmm[k];
-                g_vmm.erase(g_vmm.begin() + (long)k);
-                (void)hipDeviceSynchronize();
-                (void)hipMemUnmap(r.va, r.size);
-                (void)hipMemAddressFree(r.va, r.size);
-                (void)hipMemRelease(r.h);
-                return;
-            }
-        }
-    }
-    (void)hipFree(p);
+    return k == kAllocAuto ? kAllocContig : k;
 }
 
 template <typename T>
-hipError_t dev_alloc(T** p, size_t bytes, int kind = internal_alloc_kind(), int* got = nullptr)
+hipError_t dev_alloc(T** p, size_t bytes, int kind, int* got = nullptr)
 {
     void* v = nullptr;
     hipError_t e = hipErrorOutOfMemory;
@@ -207,12 +139,9 @@ hipError_t dev_alloc(T** p, size_t bytes, int kind = internal_alloc_kind(), int*
     if (kind == kAllocContig && bytes >= (1u << 21)) {
         e = hipExtMallocWithFlags(&v, bytes, hipDeviceMallocContiguous);
         k = kAllocContig;
-    } else if (kind == kAllocVmm && bytes >= (1u << 21)) {
-        e = vmm_alloc(&v, bytes);
-        k = kAllocVmm;
     }
     if (e != hipSuccess) {
-        (void)hipGetLastError();  // a refused request of the chosen kind falls back to hipMalloc
+        (void)hipGetLastError();  // a refused contiguous request falls back to hipMalloc
         e = hipMalloc(&v, bytes);
         k = kAllocPlain;
     }
@@ -221,6 +150,8 @@ hipError_t dev_alloc(T** p, size_t bytes, int kind = internal_alloc_kind(), int*
     *p = (T*)v;
     return e;
 }
+
+void dev_free(void* p) { (void)hipFree(p); }
 
 }  // namespace
 
@@ -251,6 +182,7 @@ struct dqdk_gpu_queue {
     uint64_t nk_max = 0;           // max_batch * E
     uint64_t scratch_words = 0;    // hist_scratch_words(nk_max) per staged slot
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
+    int alloc_kind = 0;            // device memory of the table and staging (dev_alloc)
     // Partitioned batches stage their slice-sorted keys (part2 + runs +
     // scratch, one slot each); the slice pass -- which sweeps the low-byte
     // plane of every touched slice -- runs once over hist_k staged batches,
@@ -758,6 +690,7 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                (cfg->mode == DQDK_MODE_LISTWAVE || cfg->mode == DQDK_MODE_LISTMODE ||
                 cfg->mode == DQDK_MODE_ENERGYHISTO);  // is_store_histo, src/tristan.c:65-70
     q->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    q->alloc_kind = internal_alloc_kind(q->E);
     if (const char* rs = getenv("DQDK_GPU_RAW_SYNC"))
         q->raw_sync = atoi(rs) != 0;
     if (cfg->flags & DQDK_GPU_F_HISTO_ATOMIC)
@@ -783,8 +716,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));
     if (q->histo) {
-        if ((e = dev_alloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
-            (e = dev_alloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
+        if ((e = dev_alloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->alloc_kind)) != hipSuccess ||
+            (e = dev_alloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES, q->alloc_kind)) != hipSuccess)
             return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
         if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMemset(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
@@ -815,18 +748,18 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             const size_t pe = (size_t)part_elems(nk, q->fused_elems);
             q->part2_stride = (pe + 7) & ~(size_t)7;
             q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
-            if ((e = dev_alloc(&q->d_keys, nk * 4)) != hipSuccess ||
-                (e = dev_alloc(&q->d_part1, pe * 4)) != hipSuccess ||
-                (e = dev_alloc(&q->d_part2, q->hist_k * q->part2_stride * 2)) != hipSuccess ||
-                (e = dev_alloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t))) != hipSuccess ||
-                (e = dev_alloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t))) != hipSuccess ||
+            if ((e = dev_alloc(&q->d_keys, nk * 4, q->alloc_kind)) != hipSuccess ||
+                (e = dev_alloc(&q->d_part1, pe * 4, q->alloc_kind)) != hipSuccess ||
+                (e = dev_alloc(&q->d_part2, q->hist_k * q->part2_stride * 2, q->alloc_kind)) != hipSuccess ||
+                (e = dev_alloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t), q->alloc_kind)) != hipSuccess ||
+                (e = dev_alloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t), q->alloc_kind)) != hipSuccess ||
                 (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
             // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
             const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
             const uint64_t grid = fg.grid;
             q->ovf_blk_elems = grid * ((nsuper + grid - 1) / grid) * (64 * kFWaves) * q->E;
-            if ((e = dev_alloc(&q->d_ovf_blk, q->ovf_blk_elems * 4)) != hipSuccess)
+            if ((e = dev_alloc(&q->d_ovf_blk, q->ovf_blk_elems * 4, q->alloc_kind)) != hipSuccess)
                 return cleanup((fail("hipMalloc(overflow regions)", e), -ENOMEM));
         }
     }
@@ -1158,7 +1091,7 @@ uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q)
     DevGuard dev_guard_(q->device);
     if (dev_guard_.e != hipSuccess)
         return nullptr;
-    if (!q->d_snap && dev_alloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t)) != hipSuccess) {
+    if (!q->d_snap && dev_alloc(&q->d_snap, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->alloc_kind) != hipSuccess) {
         q->d_snap = nullptr;
         return nullptr;
     }
