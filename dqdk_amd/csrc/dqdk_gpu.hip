@@ -100,10 +100,11 @@ struct Reg {
 // Device memory: plain (hipMalloc) or physically contiguous
 // (hipDeviceMallocContiguous).  UMEM images from dqdk_gpu_device_alloc are
 // contiguous (DQDK_GPU_IMAGE_ALLOC=plain: plain); the queue's table and
-// staging follow DQDK_GPU_ALLOC = plain | contig | auto (default auto:
-// contiguous from 128 events per frame, where the fused decode flushes whole
-// lines; plain below, where contiguous staging made the decode slower).
-// Measurements: DESIGN.md.
+// staging are plain (DQDK_GPU_ALLOC = plain | contig | auto, auto =
+// contiguous from 128 events per frame).  The decode's rate depends on where
+// the image and the staging land physically (9000 B: 2.27 or 2.45-2.49 ms,
+// repeatable per box and allocation pattern, but which pattern is fast
+// differs between boxes): DESIGN.md §5.
 enum AllocKind { kAllocPlain = 0, kAllocContig = 1, kAllocAuto = 2 };
 
 int alloc_kind(const char* var, int dflt)
@@ -120,7 +121,7 @@ int alloc_kind(const char* var, int dflt)
 
 int internal_alloc_kind(uint32_t E)
 {
-    static const int k = alloc_kind("DQDK_GPU_ALLOC", kAllocAuto);
+    static const int k = alloc_kind("DQDK_GPU_ALLOC", kAllocPlain);
     return k == kAllocAuto ? (E >= 128 ? kAllocContig : kAllocPlain) : k;
 }
 

@@ -1246,15 +1246,23 @@ __device__ __forceinline__ bool in_batch(uint32_t st)
     return st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
 }
 
+constexpr int kAbortLoads = 8;  // result loads in flight per thread (independent: no break between them)
+
 __global__ void __launch_bounds__(256) rx_abort_kernel(CountArgs a)
 {
     uint64_t m = a.n;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += gridDim.x * 256) {
-        const uint32_t st = a.res[i].status;
-        if (in_batch(st) && st != DQDK_RX_OK) {
-            m = i;
-            break;  // grid-stride order: later i of this thread are larger
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < a.n && m == a.n; i0 += kAbortLoads * stride) {
+        uint32_t st[kAbortLoads];
+#pragma unroll
+        for (int u = 0; u < kAbortLoads; u++) {
+            const uint32_t i = i0 + (uint32_t)u * stride;
+            st[u] = i < a.n ? a.res[i].status : (uint32_t)DQDK_RX_OK;
         }
+#pragma unroll
+        for (int u = kAbortLoads - 1; u >= 0; u--)  // grid-stride order: the smallest failing i of this thread
+            if (in_batch(st[u]) && st[u] != DQDK_RX_OK)
+                m = i0 + (uint32_t)u * stride;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1297,18 +1305,19 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
         }
     };
     // one block per CU (few blocks: every block ends in 20 device atomics on
-    // the same 20 words), four result loads in flight per thread
+    // the same 20 words), sixteen result loads in flight per thread (a 1M-frame
+    // batch in one round trip)
+    constexpr int kU = 16;
     const uint32_t stride = gridDim.x * 256;
-    for (uint32_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < a.n; i0 += 4 * stride) {
-        dqdk_gpu_rx_result_t r[4];
+    for (uint32_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < a.n; i0 += kU * stride) {
+        uint2 r[kU];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (i0 + u * stride < a.n)
-                r[u] = a.res[i0 + u * stride];
+        for (int u = 0; u < kU; u++)
+            r[u] = i0 + u * stride < a.n ? *(const uint2*)&a.res[i0 + u * stride] : make_uint2(0u, 0xffu);
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < kU; u++)
             if (i0 + u * stride < a.n)
-                count(i0 + u * stride, r[u]);
+                count(i0 + u * stride, __builtin_bit_cast(dqdk_gpu_rx_result_t, r[u]));
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -1453,6 +1462,8 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     // records path: the frame-order records of the accounted frames; fused
     // path: the decode's overflow list (usually empty)
     const uint32_t total = a.total_keys ? *a.total_keys : frames_limit(a) * a.E;
+    if (total <= blockIdx.x * (uint32_t)kP1Chunk)
+        return;  // no chunk for this block (the fused path's overflow list is usually empty)
     uint32_t* const out = a.part1 + a.part1_base;
     const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
