@@ -1951,46 +1951,63 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             stage(e0, nit);
             __syncthreads();
         }
-        for (uint32_t j = (uint32_t)wave; j < nit; j += kNI * kWavesS) {
-            // an item's run parameters are wave-uniform: scalar registers, and
-            // a buffer descriptor per item whose extent ends at the run's last
-            // dword (so the loads need no per-lane bound)
-            uint32_t klo[kNI], khi[kNI], dlo[kNI];
-            __amdgpu_buffer_rsrc_t src[kNI];
+        // a group = the kNI items j, j + kWavesS, ... of one wave.  Item run
+        // parameters are wave-uniform and re-read from LDS where needed, so
+        // nothing but the loaded dwords is live across a group's loads
+        // (64 VGPRs: 4 blocks per CU).  Issuing the next group's loads before
+        // counting this one's measured slower.
+        constexpr uint32_t kGrp = kNI * kWavesS;
+        auto run = [&](uint32_t jj, uint32_t& klo, uint32_t& khi) {
+            const bool v = jj < nit;
+            const uint32_t jc = v ? jj : 0u;
+            klo = v ? rfl(sl.s_lo[jc]) : 0u;
+            khi = v ? rfl(sl.s_hi[jc]) : 0u;
+        };
+        // a buffer descriptor per item whose extent ends at the run's last
+        // dword (so the loads need no per-lane bound); items start at
+        // multiples of kBucketAlign keys: dword-aligned
+        auto issue = [&](uint32_t j, uint32_t p0, uint32_t (&w)[kNI][kKG]) -> uint32_t {
             uint32_t steps = 0;
 #pragma unroll
             for (int q = 0; q < kNI; q++) {
                 const uint32_t jj = j + q * kWavesS;
-                const bool v = jj < nit;
-                const uint32_t jc = v ? jj : 0u;
-                klo[q] = v ? rfl(sl.s_lo[jc]) : 0u;
-                khi[q] = v ? rfl(sl.s_hi[jc]) : 0u;
-                dlo[q] = klo[q] >> 1;
-                const uint32_t dhi = (khi[q] + 1) >> 1;
-                // items start at multiples of kBucketAlign keys: dword-aligned
+                uint32_t klo, khi;
+                run(jj, klo, khi);
+                const uint32_t jc = jj < nit ? jj : 0u;
+                const uint32_t dlo = klo >> 1, dhi = (khi + 1) >> 1;
                 const uint16_t* base = a.part2 + (uint64_t)rfl(sl.s_k[jc]) * a.part2_stride +
                                        (uint64_t)rfl(sl.s_base[jc]) * kBucketAlign;
-                src[q] = uniform_rsrc(base, (uint64_t)dhi * 4u);
-                steps = max(steps, dhi - dlo[q]);
+                const __amdgpu_buffer_rsrc_t src = uniform_rsrc(base, (uint64_t)dhi * 4u);
+#pragma unroll
+                for (int g = 0; g < kKG; g++)
+                    w[q][g] = __builtin_amdgcn_raw_buffer_load_b32(src, (dlo + p0 + 64 * g + lane) * 4u, 0, 0);
+                steps = max(steps, dhi - dlo);
             }
-            for (uint32_t p0 = 0; p0 < steps; p0 += 64 * kKG) {
-                uint32_t w[kNI][kKG];
+            return steps;
+        };
+        auto count = [&](uint32_t j, uint32_t p0, const uint32_t (&w)[kNI][kKG]) {
 #pragma unroll
-                for (int q = 0; q < kNI; q++)
+            for (int q = 0; q < kNI; q++) {
+                uint32_t klo, khi;
+                run(j + q * kWavesS, klo, khi);
+                const uint32_t dlo = klo >> 1;
 #pragma unroll
-                    for (int g = 0; g < kKG; g++)
-                        w[q][g] = __builtin_amdgcn_raw_buffer_load_b32(src[q], (dlo[q] + p0 + 64 * g + lane) * 4u, 0,
-                                                                        0);
-#pragma unroll
-                for (int q = 0; q < kNI; q++)
-#pragma unroll
-                    for (int g = 0; g < kKG; g++) {
-                        const uint32_t k0 = 2 * (dlo[q] + p0 + 64 * g + lane);  // key index of the low half
-                        if (k0 >= klo[q] && k0 < khi[q])
-                            slice_count<kPacked>(h, w[q][g] & 0xffffu);
-                        if (k0 + 1 >= klo[q] && k0 + 1 < khi[q])
-                            slice_count<kPacked>(h, w[q][g] >> 16);
-                    }
+                for (int g = 0; g < kKG; g++) {
+                    const uint32_t k0 = 2 * (dlo + p0 + 64 * g + lane);  // key index of the low half
+                    if (k0 >= klo && k0 < khi)
+                        slice_count<kPacked>(h, w[q][g] & 0xffffu);
+                    if (k0 + 1 >= klo && k0 + 1 < khi)
+                        slice_count<kPacked>(h, w[q][g] >> 16);
+                }
+            }
+        };
+        for (uint32_t j = (uint32_t)wave; j < nit; j += kGrp) {
+            uint32_t w[kNI][kKG];
+            const uint32_t steps = issue(j, 0, w);
+            count(j, 0, w);
+            for (uint32_t p0 = 64 * kKG; p0 < steps; p0 += 64 * kKG) {  // runs longer than one pass (rare)
+                issue(j, p0, w);
+                count(j, p0, w);
             }
         }
     }
@@ -2038,7 +2055,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     }
 }
 
-__global__ void __launch_bounds__(kSliceThreads) rx_slice_histo_kernel(HistoArgs a)
+__global__ void __launch_bounds__(kSliceThreads, 8) rx_slice_histo_kernel(HistoArgs a)  // 4 blocks per CU
 {
     __shared__ __attribute__((aligned(16))) uint32_t h[(1 << kSliceBits) / 2];
     __shared__ SliceLds sl;
