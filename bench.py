@@ -280,9 +280,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         # records path: keys read + bucket runs written; fused path: the overflow list only (~0)
         "rx_part1": 8 * K if pass_records else 0,
         # fused path: the per-bucket scans of the decode's piece sizes (checksum-failed
-        # frames taken back: none in the timed workload)
+        # frames taken back and overflow keys grouped: none in the timed workload)
         "rx_fixup": 284 * 256 * 4 + 284 * 257 * 4,
-        "rx_hist_prep": 12 * 288,
         "rx_part2": 6 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
@@ -321,8 +320,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                                                      0, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
         pattern["per_frame"] = round(n * (fbytes + 4 * E) / (ms.value * 1e-3) / 1e9, 1)
 
-    hist_kernels = [k for k in ("rx_histo_atomic", "rx_fixup", "rx_part1", "rx_hist_prep", "rx_part2",
-                                "rx_slice_histo", "rx_slice_heavy") if k in st]
+    hist_kernels = [k for k in ("rx_histo_atomic", "rx_fixup", "rx_part1", "rx_part2", "rx_slice_histo",
+                                "rx_slice_heavy") if k in st]
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["ms_per_batch"] for k in hist_kernels)

@@ -71,9 +71,12 @@ struct DevGuard {
         return fail("hipSetDevice", dev_guard_.e)
 
 constexpr int kStages = DQDK_GPU_TIMING_STAGES;
+// (rx_fixup: on the fused path, the launch of rx_part1_kernel that takes the
+// decode's piece scans, checksum-failed frames and overflow list; stage 5 is
+// unused since rx_part2 derives its items itself)
 enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy, kStFixup };
-const char* const kStageNames[kStages] = {"rx_decode",    "rx_abort", "rx_count",       "rx_histo_atomic",
-                                          "rx_part1",     "rx_hist_prep", "rx_part2",   "rx_slice_histo",
+const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",       "rx_histo_atomic",
+                                          "rx_part1",  "(unused)", "rx_part2",       "rx_slice_histo",
                                           "rx_slice_heavy", "rx_fixup"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
 
@@ -177,11 +180,11 @@ struct dqdk_gpu_queue {
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
     uint32_t* d_fix = nullptr;     // fused path: decoded frames that failed afterwards (max_batch)
-    uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions
+    uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions (in d_part1's rx_part1 region)
     uint64_t ovf_blk_elems = 0;
     uint64_t fused_elems = 0;      // fused path: pieces region (0: the fused path is off)
     uint64_t nk_max = 0;           // max_batch * E
-    uint64_t scratch_words = 0;    // hist_scratch_words(nk_max) per staged slot
+    uint64_t scratch_words = 0;    // kHistScratchWords per staged slot
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
     int alloc_kind = 0;            // device memory of the table and staging (dev_alloc)
     // Partitioned batches stage their slice-sorted keys (part2 + runs +
@@ -271,9 +274,13 @@ constexpr uint64_t kPartitionMinKeys = 4u << 20;
 #ifndef DQDK_HIST_SLICE_EVENTS
 #define DQDK_HIST_SLICE_EVENTS 49152
 #endif
-constexpr size_t kHistKMax = DQDK_HIST_KMAX;                  // staged batches per slice pass, at most
+#ifndef DQDK_HIST_STAGE_MB
+#define DQDK_HIST_STAGE_MB 16384
+#endif
+constexpr size_t kHistKMax = DQDK_HIST_KMAX;  // staged batches per slice pass, at most
 static_assert(kHistKMax <= (size_t)kSliceMaxSlots, "the slice pass indexes staged batches in registers");
 constexpr size_t kHistSliceEvents = DQDK_HIST_SLICE_EVENTS;  // staged events per slice, target
+constexpr size_t kHistStageBytes = (size_t)DQDK_HIST_STAGE_MB << 20;  // staging budget of a queue
 
 bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)
 {
@@ -290,12 +297,11 @@ int hist_flush(dqdk_gpu_queue* q)
     HistoArgs ha{};
     ha.hist = q->d_hist;
     ha.lo = q->d_lo;
-    ha.scratch = q->d_hscratch;  // slot 0 also holds the heavy-slice list
+    ha.scratch = q->d_hscratch;
     ha.part2 = q->d_part2;
     ha.runs = q->d_runs;
     ha.nslots = q->hist_pending;
     ha.scratch_stride = (uint32_t)q->scratch_words;
-    ha.heavy_off = (uint32_t)heavy_off(q->nk_max);
     ha.part2_stride = q->part2_stride;
     ha.runs_stride = q->runs_stride;
     q->hist_pending = 0;
@@ -443,7 +449,6 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ha.part1 = q->d_part1;
         ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
         ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
-        ha.heavy_off = (uint32_t)heavy_off(q->nk_max);
         if (fused) {
             ha.keys = q->d_keys;                    // the overflow list
             ha.total_keys = slot_scratch + kOffOvfN;
@@ -458,10 +463,6 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             StageTimer t(q, kStAtomic);
             hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
         } else {
-            if (fused) {
-                StageTimer t(q, kStFixup);  // piece scans, then (usually) an empty list
-                hipLaunchKernelGGL(rx_fixup_kernel, dim3((kL1Buckets + 3) / 4), dim3(256), 0, q->stream, ra, ha);
-            }
             const uint64_t nkeys = (uint64_t)n * q->E;
             const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
             const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
@@ -469,12 +470,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
                                                         (uint32_t)q->cu_count * 2u);
             {
-                StageTimer t(q, kStPart1);  // fused: groups the overflow list (usually empty)
-                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ha);
-            }
-            {
-                StageTimer t(q, kStPrep);
-                hipLaunchKernelGGL(rx_hist_prep_kernel, dim3(1), dim3(1024), 0, q->stream, ha);
+                // fused: the decode's piece scans and checksum-failed frames,
+                // then the overflow list (usually empty), timed as "rx_fixup"
+                StageTimer t(q, fused ? kStFixup : kStPart1);
+                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ra, ha);
             }
             {
                 StageTimer t(q, kStPart2);
@@ -725,30 +724,38 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
+            q->nk_max = nk;
+            q->scratch_words = kHistScratchWords;
+            // part2: item i of a staged batch at [i * kPartChunk, + keys)
+            q->part2_stride = (size_t)max_items(nk) * kPartChunk;
+            q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
             // Stage up to kHistKMax batches per slice pass, as many as keep a
             // slice of uniformly spread events at about 3/4 of the 65535
             // events of the packed-u16 form (kHistSliceEvents; the low-byte
             // sweep is amortised over them, a fuller slice still takes the u32
-            // form); DQDK_GPU_F_HISTO_EAGER: a pass per batch.
+            // form) and fit the staging budget; DQDK_GPU_F_HISTO_EAGER: a
+            // pass per batch.
             const size_t per_slice = (nk + kSlices - 1) / kSlices;
+            const size_t slot_bytes = q->part2_stride * 2 + q->runs_stride * 2 + q->scratch_words * 4;
             q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
                             ? 1u
                             : (uint32_t)std::max<size_t>(
-                                  1, std::min<size_t>(kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1)));
-            // part1/part2 hold the fused decode's pieces, then rx_part1's region
-            // (records / overflow); slots start 16-B aligned (part2's 16-B
-            // stores and the slice gather's dword loads assume it)
-            q->nk_max = nk;
-            q->scratch_words = hist_scratch_words(nk);
-            // the fused pieces at max_batch bound those of any smaller batch;
-            // gathered items address them in 32-bit byte offsets per bucket
+                                  1, std::min({kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1),
+                                               kHistStageBytes / slot_bytes}));
+            // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
             const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->cu_count);
+            const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
+            q->ovf_blk_elems = fg.grid * ((nsuper + fg.grid - 1) / fg.grid) * (64 * kFWaves) * q->E;
+            // part1 holds the fused decode's pieces, then rx_part1's region
+            // (records / overflow), which also backs the decode's overflow
+            // regions (dead before rx_part1 writes it); the fused pieces at
+            // max_batch bound those of any smaller batch; gathered items
+            // address them in 32-bit byte offsets per bucket
             q->fused_elems = fg.region * 4u < (1ull << 31) && (uint64_t)kL1Buckets * fg.region < (1ull << 32)
                                  ? (uint64_t)kL1Buckets * fg.region
                                  : 0u;
-            const size_t pe = (size_t)part_elems(nk, q->fused_elems);
-            q->part2_stride = (pe + 7) & ~(size_t)7;
-            q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
+            const size_t pe = (size_t)std::max<uint64_t>(part_elems(nk, q->fused_elems),
+                                                         q->fused_elems + q->ovf_blk_elems);
             if ((e = dev_alloc(&q->d_keys, nk * 4, q->alloc_kind)) != hipSuccess ||
                 (e = dev_alloc(&q->d_part1, pe * 4, q->alloc_kind)) != hipSuccess ||
                 (e = dev_alloc(&q->d_part2, q->hist_k * q->part2_stride * 2, q->alloc_kind)) != hipSuccess ||
@@ -756,12 +763,7 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                 (e = dev_alloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t), q->alloc_kind)) != hipSuccess ||
                 (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                 return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
-            // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
-            const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
-            const uint64_t grid = fg.grid;
-            q->ovf_blk_elems = grid * ((nsuper + grid - 1) / grid) * (64 * kFWaves) * q->E;
-            if ((e = dev_alloc(&q->d_ovf_blk, q->ovf_blk_elems * 4, q->alloc_kind)) != hipSuccess)
-                return cleanup((fail("hipMalloc(overflow regions)", e), -ENOMEM));
+            q->d_ovf_blk = q->d_part1 + q->fused_elems;
         }
     }
     *out = q;
@@ -825,7 +827,6 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     dev_free(q->d_runs);
     dev_free(q->d_hscratch);
     (void)hipFree(q->d_fix);
-    dev_free(q->d_ovf_blk);
     (void)hipFree(q->d_desc);
     (void)hipFree(q->d_res);
     (void)hipFree(q->d_raw_blk);

@@ -15,15 +15,17 @@
  * K3 histogram accumulation of the keys of accounted OK frames (the relaxed
  *    atomic increment of src/tristan.c:243), two interchangeable forms:
  *    - rx_histo_atomic: one device-scope atomic per event (small batches);
- *    - partitioned: rx_part1 (keys -> 284 buckets of 2^21 bins, long runs),
- *      rx_part2 (each 16K-key chunk of a bucket sorted by 16K-bin slice in
- *      LDS, written back as u16 slice-local keys + run offsets),
- *      rx_slice_histo (gathers the slice's runs, packed-u16 LDS histogram,
- *      one coalesced read-modify-write of the slice's 16 KB low-byte plane,
- *      carries of 256 into the u32 base plane; slices with more than 65535
- *      events are listed and redone with u32 LDS bins by rx_slice_heavy).  The table is held as
- *      value = base[bin] + low[bin] (mod 2^32): the same values as the
- *      reference's u32 table, with a 4x smaller per-batch sweep.
+ *    - partitioned: keys grouped by L1 bucket of 2^21 bins (the fused decode's
+ *      per-block pieces, or rx_part1 over frame-order records / the fused
+ *      decode's overflow list), rx_part2 (each 16K-key chunk of a bucket
+ *      sorted by 16K-bin slice in LDS, written as u16 slice-local keys + run
+ *      offsets), rx_slice_histo (gathers the slice's runs over the staged
+ *      batches, packed-u16 LDS histogram, one coalesced read-modify-write of
+ *      the slice's 16 KB low-byte plane, carries of 256 into the u32 base
+ *      plane; slices with more than 65535 events are listed and redone with
+ *      u32 LDS bins by rx_slice_heavy).  The table is held as value =
+ *      base[bin] + low[bin] (mod 2^32): the same values as the reference's
+ *      u32 table, with a 4x smaller per-pass sweep.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -79,18 +81,18 @@ constexpr int kOffFixN = 578;       // fused path: decoded frames whose final st
 constexpr int kZeroWords = 584;
 constexpr int kMaxFusedGrid = 256;  // fused decode blocks (one per CU)
 constexpr int kOffOff1 = kZeroWords;  // [kL1Buckets + 1] bucket starts of rx_part1's output (prep)
-constexpr int kOffIstart = kOffOff1 + 288;  // [kL1Buckets + 1] first part2 item of each bucket; [284] = items (prep)
+constexpr int kOffIstart = kOffOff1 + 288;  // [kL1Buckets + 1] first part2 item of each bucket; [284] = items (rx_part2)
 // fused path: keys of each (bucket, block) piece [kL1Buckets][kMaxFusedGrid] (decode),
 // and their exclusive scans per bucket [kL1Buckets][kMaxFusedGrid + 1] (prep)
 constexpr int kOffPieceN = kOffIstart + 288;
 constexpr int kOffPiecePre = kOffPieceN + kL1Buckets * kMaxFusedGrid;
-constexpr int kOffItems = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);  // [2 * items]: (part2 index, keys) (prep)
+constexpr int kOffEnd = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);
 constexpr int kSegsPerBucket = 2;  // fused: the bucket's pieces (one gathered sequence), then rx_part1's overflow run
 // items of a batch of nk keys: one per started 16K-key chunk of each segment
 __host__ __device__ constexpr uint64_t max_items(uint64_t nk) { return nk / 16384 + (uint64_t)kL1Buckets * kSegsPerBucket + 1; }
-// words of one slot: the fixed part, the item table, the heavy-slice list
-__host__ __device__ constexpr uint64_t hist_scratch_words(uint64_t nk) { return kOffItems + 2 * max_items(nk) + kSlices; }
-__host__ __device__ constexpr uint64_t heavy_off(uint64_t nk) { return kOffItems + 2 * max_items(nk); }
+constexpr int kOffHeavyList = kOffEnd;  // [kSlices] (slot 0 of a slice pass) slices redone in u32
+// u32 words of one staged slot's scratch
+constexpr uint64_t kHistScratchWords = kOffHeavyList + kSlices;
 constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a segment)
 
 // Fused decode (rx_decode_fused): 1024-thread blocks, one per CU, persistent.
@@ -174,14 +176,13 @@ struct HistoArgs {
     uint32_t* scratch;  // kHistScratchWords
     uint32_t* part1;    // keys grouped by bucket (rx_part1's region starts at part1_base)
     uint64_t part1_base;  // first element of rx_part1's output (0, or after the fused pieces)
-    uint16_t* part2;    // slice-local keys (key & 16383) at the same indices, each 16K item sorted by slice
+    uint16_t* part2;    // item i's slice-sorted u16 bins ((key & 16383) << 2) at [i * kPartChunk, + keys)
     uint16_t* runs;     // [items][kItemOffs] slice run starts inside each item
     const uint32_t* total_keys;  // rx_part1 input length on the device (overflow list), or null: limit * E
     uint32_t fused;     // the keys are the fused decode's pieces + rx_part1's run of its overflow
     uint32_t fgrid;     // fused: decode blocks (pieces per bucket)
     uint32_t piece_cap;
     uint64_t region;
-    uint32_t heavy_off; // scratch word of the heavy-slice list
     // the slice pass runs over nslots staged batches: batch k's scratch,
     // part2 keys and run offsets sit k strides (elements) after the first
     uint32_t nslots;
@@ -192,12 +193,10 @@ struct HistoArgs {
 __global__ void rx_decode_kernel(RxArgs a);
 template <int kLdAux, bool kLines>
 __global__ void rx_decode_fused_kernel(RxArgs a);
-__global__ void rx_fixup_kernel(RxArgs a, HistoArgs h);
 __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);
-__global__ void rx_part1_kernel(HistoArgs a);
-__global__ void rx_hist_prep_kernel(HistoArgs a);
+__global__ void rx_part1_kernel(RxArgs ra, HistoArgs a);
 template <int kLdAux>
 __global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);

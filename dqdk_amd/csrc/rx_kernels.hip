@@ -368,6 +368,19 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x)
     return rdl(x, 15) + rdl(x, 31) + rdl(x, 47) + rdl(x, 63);
 }
 
+// inclusive prefix sum over the wave: rows by DPP shifts, then rows 1-3
+// take the earlier rows' totals by row broadcasts (no LDS round trips)
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes)
 {
     // SRD from readfirstlane'd halves so hipcc can prove it uniform
@@ -1144,7 +1157,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
             a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
     }
-    // the keys still staged, then the piece sizes for rx_hist_prep
+    // the keys still staged, then the piece sizes for rx_part1 / rx_part2
     lds_barrier();
     fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, true);
     {
@@ -1181,13 +1194,15 @@ template __global__ void rx_decode_fused_kernel<2, true>(RxArgs);
 // Frames the fused decode staged but whose final status is not OK: subtract
 // their events from the table (u32 wrap: +1 then -1 leaves every bin exact).
 // Event bytes are read as the decode read them (zeros at or past umem_size).
-__global__ void __launch_bounds__(256) rx_fixup_kernel(RxArgs a, HistoArgs h)
+// Runs as rx_part1's prologue on the fused path (a launch of its own cost
+// more than its work); gw / nw: the calling wave's index / the grid's waves.
+__device__ __forceinline__ void fused_fixup(const RxArgs& a, const HistoArgs& h, uint32_t gw, uint32_t nw)
 {
     const uint32_t nfix = a.scratch[kOffFixN];
     const int lane = threadIdx.x & 63;
     // first, one wave per bucket: the exclusive scan of its piece sizes
-    // (rx_hist_prep's segment sizes, rx_part2's piece starts)
-    for (uint32_t b = (blockIdx.x * 256 + threadIdx.x) >> 6; b < (uint32_t)kL1Buckets; b += (gridDim.x * 256) >> 6) {
+    // (rx_part2's segment sizes and piece starts)
+    for (uint32_t b = gw; b < (uint32_t)kL1Buckets; b += nw) {
         const uint32_t* cn = a.scratch + kOffPieceN + b * kMaxFusedGrid;
         uint32_t* pre = a.scratch + kOffPiecePre + b * (kMaxFusedGrid + 1);
         uint32_t v[4], sum = 0;
@@ -1215,7 +1230,7 @@ __global__ void __launch_bounds__(256) rx_fixup_kernel(RxArgs a, HistoArgs h)
         if (lane == 63)
             pre[h.fgrid] = incl;
     }
-    for (uint32_t k = (blockIdx.x * 256 + threadIdx.x) >> 6; k < nfix; k += (gridDim.x * 256) >> 6) {
+    for (uint32_t k = gw; k < nfix; k += nw) {
         const uint32_t i = a.fix[k];
         const uint64_t addr = a.desc[i].addr;
         const uint64_t ihl_at = addr + 14;
@@ -1435,10 +1450,6 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #define DQDK_P1_PIPE 1
 #endif
 constexpr bool kP1Pipe = DQDK_P1_PIPE;  // part1 loads chunk c+1 while chunk c is written out
-#ifndef DQDK_P2_PIPE
-#define DQDK_P2_PIPE 1
-#endif
-constexpr bool kP2Pipe = DQDK_P2_PIPE;  // part2 loads item i+1 while item i is written out
 
 // Level 1: keys (frame order) -> part1, grouped by bucket = key >> 21.
 // A block stages kP1Chunk keys in LDS sorted by bucket, reserves each
@@ -1451,8 +1462,10 @@ constexpr bool kP2Pipe = DQDK_P2_PIPE;  // part2 loads item i+1 while item i is 
 // after the scatter.  One 32K-key chunk per block (128 KB of LDS, one block
 // per CU) halves the reservations per key of a 16K chunk and doubles the
 // average run written per bucket.
-__global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(HistoArgs a)
+__global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArgs ra, HistoArgs a)
 {
+    if (a.fused)  // the fused decode's piece scans and checksum-failed frames
+        fused_fixup(ra, a, (blockIdx.x * kP1Threads + threadIdx.x) >> 6, (gridDim.x * kP1Threads) >> 6);
     __shared__ uint32_t stage[kP1Chunk];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t lcnt[kL1Buckets];
@@ -1530,277 +1543,270 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(Histo
     }
 }
 
-// Segments -> part2 items, once per batch.  A segment is a sequence of keys
-// of one L1 bucket: records path, rx_part1's run of the bucket (starts = scan
-// of the decode's upper bounds); fused path, the bucket's pieces (one per
-// decode block, adjacent in the fused region, gathered through the scan of
-// their sizes written here) then rx_part1's run of its overflow keys.  Every
-// started 16K-key chunk of a segment is a part2 item; items are numbered
-// bucket by bucket, and the item table holds each item's part2 index (in
-// units of kBucketAlign keys: part1/part2 may pass 2^32 keys) and key count.
-// A gathered item's part2 index is its bucket's region start + its offset in
-// the bucket's key sequence, which is also where rx_part2 finds its pieces.
-__global__ void __launch_bounds__(1024) rx_hist_prep_kernel(HistoArgs a)
+// Level 2: each part2 item = one 16K-key chunk of a segment, sorted by slice
+// ((key >> 14) & 127) in LDS and written to part2 [item * 16K, + keys) as u16
+// (the key's low 16 bits: readers mask off bits 14-15, the slice's), with the
+// run starts of its 128 slices.  A segment is a sequence of keys of one
+// L1 bucket: records path, rx_part1's run of the bucket; fused path, the
+// bucket's pieces (one per decode block, adjacent in the fused region,
+// gathered through the scan of their sizes that rx_part1's prologue wrote),
+// then rx_part1's run of the bucket's overflow keys.  Items are numbered
+// segment by segment; every block derives the segment table and the item
+// starts itself (a prologue over L2-resident counts, in place of a launch of
+// its own), and block 0 publishes each bucket's first item for the slice pass.
+//
+// Per key: one buffer load, one returning LDS add (counts step by 2, so the
+// returned rank is the key's byte offset inside its slice run), the rank
+// through LDS, one LDS read of the run start, one u16 LDS store.  The next
+// item's keys load while this one is written out.  The barriers hand off LDS
+// data only (global reads are read-only inputs, global writes are not read
+// back by the block): lds_barrier() keeps the next item's key loads in flight
+// across them.
+template <int kLdAux>
+__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     constexpr int kMaxSeg = kL1Buckets * kSegsPerBucket;
+    constexpr int kPWaves = kPartThreads / 64;
+    constexpr uint32_t kWaveSlots = (uint32_t)kPartChunk / kPWaves;  // 1024 key slots per wave
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
+    // counters / run starts of 2 * kSubs slices: bit 21 of a key (the bucket's
+    // low bit) is part of its counter index, so the item's slices use one half
+    // and the other half holds the dummy slice of the slots past the item
+    __shared__ __attribute__((aligned(16))) uint32_t lcnt[2 * kSubs];
+    __shared__ __attribute__((aligned(16))) uint32_t loff[2 * kSubs];
+    __shared__ uint32_t rnk[kPartKeysPerThread / 2 * kPartThreads];  // count() -> scatter()
+    __shared__ uint32_t prow[2][kMaxFusedGrid + 1];
+    __shared__ uint32_t s_cnt[kMaxSeg], s_base8[kMaxSeg], ist[kMaxSeg + 1];
     __shared__ uint32_t off1[kL1Buckets + 1];
-    __shared__ uint32_t ist[kMaxSeg + 1];
-    __shared__ uint32_t ptot[kL1Buckets];
-    __shared__ uint32_t wsum[16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint32_t wsum[kPWaves];
+    const int tid = threadIdx.x;
+    const uint32_t lane = (uint32_t)tid & 63u, wave = rfl((uint32_t)tid >> 6);
+    const bool fused = a.fused != 0;
+    const uint32_t nseg = fused ? (uint32_t)kMaxSeg : (uint32_t)kL1Buckets;
+
+    // ---- prologue: segments (key count, part2 index) and their first items ----
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
-    if (a.fused && tid < kL1Buckets)  // (rx_fixup scanned the piece sizes)
-        ptot[tid] = a.scratch[kOffPiecePre + tid * (kMaxFusedGrid + 1) + a.fgrid];
+    if (tid < 2 * kSubs)
+        lcnt[tid] = 0;
     __syncthreads();
-    if (tid <= kL1Buckets)
-        a.scratch[kOffOff1 + tid] = (uint32_t)a.part1_base + off1[tid];
-    const int S = a.fused ? kSegsPerBucket : 1;
-    const int nseg = kL1Buckets * S;
-    auto seg = [&](int t, uint32_t& cnt, uint64_t& base) {
-        const int b = t / S, g = t - b * S;
-        if (!a.fused || g == 1) {
-            cnt = a.scratch[kOffCur1 + b];
+    uint32_t nit = 0;
+    if ((uint32_t)tid < nseg) {
+        const uint32_t b = fused ? (uint32_t)tid >> 1 : (uint32_t)tid;
+        uint32_t c;
+        uint64_t base;
+        if (!fused || (tid & 1)) {  // rx_part1's run of the bucket
+            c = a.scratch[kOffCur1 + b];
             base = a.part1_base + off1[b];
-        } else {
-            cnt = ptot[b];
+        } else {                    // the bucket's pieces
+            c = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + a.fgrid];
             base = (uint64_t)b * a.region;
         }
-    };
-    // exclusive scan of items per segment: thread t owns segments 3t .. 3t+2
-    uint32_t v[3], sum = 0;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int t = 3 * tid + j;
-        uint32_t c = 0;
-        uint64_t bs;
-        if (t < nseg)
-            seg(t, c, bs);
-        v[j] = (c + kPartChunk - 1) / kPartChunk;
-        sum += v[j];
+        s_cnt[tid] = c;
+        s_base8[tid] = (uint32_t)(base / kBucketAlign);
+        nit = (c + kPartChunk - 1) / kPartChunk;
     }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = __shfl_up(incl, o);
-        if (lane >= o)
-            incl += x;
-    }
+    const uint32_t incl = wave_incl_scan_dpp(nit);
     if (lane == 63)
         wsum[wave] = incl;
     __syncthreads();
     uint32_t woff = 0;
-    for (int w = 0; w < wave; w++)
+    for (uint32_t w = 0; w < wave; w++)
         woff += wsum[w];
-    uint32_t run = woff + incl - sum;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int t = 3 * tid + j;
-        if (t <= nseg)
-            ist[t] = run;
-        run += v[j];
-    }
+    if ((uint32_t)tid <= nseg)
+        ist[tid] = woff + incl - nit;
     __syncthreads();
-    if (tid <= kL1Buckets)
-        a.scratch[kOffIstart + tid] = ist[tid * S];
-    // item table: with many items per segment (9000 B: ~126) a wave per
-    // segment, lanes on consecutive items (coalesced stores); with few
-    // (1500 B: ~21) a thread per segment (36 segments per wave in a row
-    // would cost more than the scattered stores)
-    uint32_t* items = a.scratch + kOffItems;
-    auto put = [&](uint32_t it, uint64_t bs, uint32_t c, uint32_t j) {
-        items[2 * it] = (uint32_t)((bs + (uint64_t)j * kPartChunk) / kBucketAlign);
-        items[2 * it + 1] = min(c - j * (uint32_t)kPartChunk, (uint32_t)kPartChunk);
-    };
-    if (ist[nseg] > 32u * (uint32_t)nseg) {
-        for (int t = wave; t < nseg; t += 16) {
-            uint32_t c;
-            uint64_t bs;
-            seg(t, c, bs);
-            const uint32_t i0 = ist[t], ni = (c + kPartChunk - 1) / kPartChunk;
-            for (uint32_t j = (uint32_t)lane; j < ni; j += 64)
-                put(i0 + j, bs, c, j);
-        }
-    } else {
-        for (int t = tid; t < nseg; t += 1024) {
-            uint32_t c;
-            uint64_t bs;
-            seg(t, c, bs);
-            for (uint32_t j = 0, it = ist[t]; j * (uint32_t)kPartChunk < c; j++, it++)
-                put(it, bs, c, j);
-        }
-    }
-}
+    const uint32_t nitems = rfl(ist[nseg]);
+    if (blockIdx.x == 0 && tid <= kL1Buckets)
+        a.scratch[kOffIstart + tid] = ist[fused ? 2 * tid : tid];
 
-// Level 2: each item = one 16K-key chunk of one bucket's part1 run, sorted
-// by slice ((key >> 14) & 127) in LDS and written back in place as u16
-// slice-local keys, with the run starts of its 128 slices.
-// part2's barriers hand off LDS data only (its global reads are read-only
-// inputs, its global writes are not read back by the block): lds_barrier()
-// keeps the next item's key loads in flight across them, where
-// __syncthreads() would wait for every load and store (vmcnt(0))
-#ifdef DQDK_P2_SYNCTHREADS
-#define P2_BARRIER __syncthreads
-#else
-#define P2_BARRIER lds_barrier
-#endif
-// kLdAux: the key loads' cache policy (2 = non-temporal: each key is read
-// once; measured faster below 128 events per frame, slower from 128 on)
-template <int kLdAux>
-__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
-{
-    __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
-    __shared__ uint32_t lcnt[kSubs], loff[kSubs + 1];
-    __shared__ uint32_t prow[2][kMaxFusedGrid + 1];
-    const int tid = threadIdx.x;
-    const uint32_t nitems = a.scratch[kOffIstart + kL1Buckets];
-    const uint32_t* items = a.scratch + kOffItems;
-    uint32_t key[kPartKeysPerThread];
-    // item -> its keys [base, base + nk) in part1/part2 (the prep's item
-    // table); load() puts them in key[] (out-of-range lanes read 0, dropped below)
-    auto geo = [&](uint32_t item, uint32_t& nk, uint64_t& base) {
-        base = (uint64_t)items[2 * item] * kBucketAlign;
-        nk = items[2 * item + 1];
+    // ---- an item's geometry (wave-uniform): its segment is the number of
+    // segment starts ist[1..nseg) at or below it (nine ballots) ----
+    struct Item {
+        uint32_t s0;     // first key of the item in its segment
+        uint32_t nk;     // keys
+        uint32_t b;      // bucket
+        uint32_t base8;  // part2 index / kBucketAlign
+        bool gath;       // fused pieces (else one contiguous run)
     };
-    // a gathered item (fused path): its bucket's piece starts go to prow[pb]
-    // (then a barrier), and each key's piece is found there
-    auto gathered = [&](uint64_t base) { return a.fused && base < a.part1_base; };
-    auto stage_pieces = [&](uint64_t base, int pb) {
-        if (gathered(base)) {
-            const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
-            if ((uint32_t)tid <= a.fgrid)
-                prow[pb][tid] = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + tid];
+    // (the lane-derived addresses are opaque to the compiler: hoisted out of
+    // the item loop they would stay live, and spill, across it)
+    auto geo = [&](uint32_t item) {
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t t = 0;
+#pragma unroll
+        for (int m = 0; m < (kMaxSeg + 63) / 64; m++) {
+            const uint32_t k = 1u + ln + 64u * (uint32_t)m;
+            t += (uint32_t)__builtin_popcountll(__ballot(k < nseg && ist[min(k, (uint32_t)kMaxSeg)] <= item));
         }
+        Item g;
+        g.s0 = (item - rfl(ist[t])) * (uint32_t)kPartChunk;
+        g.nk = min(rfl(s_cnt[t]) - g.s0, (uint32_t)kPartChunk);
+        g.b = fused ? t >> 1 : t;
+        g.gath = fused && !(t & 1u);
+        g.base8 = rfl(s_base8[t]) + g.s0 / kBucketAlign;
+        return g;
     };
-    // key slots: wave w takes the item's keys [1024w, 1024w + 1024), 64 per
-    // load (slot(j) = 1024w + 64j + lane), so a gathered item's wave crosses
-    // a piece boundary about once: the piece lookup is one uniform compare
-    // per load, with a per-lane walk only where a boundary falls inside it
-    const uint32_t lane = (uint32_t)tid & 63u, wq0 = (uint32_t)tid & ~63u;  // wq0 = 1024 * wave / 16
-    auto slot = [&](int j) { return wq0 * 16u + 64u * (uint32_t)j + lane; };
-    auto load = [&](uint64_t base, uint32_t nk, int pb) {
-        if (gathered(base)) {
-            const uint32_t b = (uint32_t)base / (uint32_t)a.region;  // (base < part1_base < 2^32)
-            const uint32_t S = (uint32_t)base - b * (uint32_t)a.region;
-            const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)b * a.region, a.region * 4u);
+    // a gathered item: its bucket's piece starts (then a barrier)
+    auto stage_pieces = [&](const Item& g, int pb) {
+        if (g.gath && (uint32_t)tid <= a.fgrid)
+            prow[pb][tid] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + tid];
+    };
+    // key slots: wave w takes the item's slots [1024w, 1024w + 1024), 64 per
+    // load (slot(j) = 1024w + 64j + lane)
+    uint32_t key[kPartKeysPerThread];
+    auto load = [&](const Item& g, int pb) {
+        const uint32_t w0 = wave * kWaveSlots;
+        if (g.gath) {
+            // key k of the bucket's sequence lies in piece p (pr[p] <= k <
+            // pr[p + 1]) at region slot p * cap + k - pr[p].  Lane state: t =
+            // start of the next piece - the lane's first key, u = byte offset
+            // of that key were it in the lane's current piece (a load's offset
+            // is u + 256 j); the state moves only where a load crosses a piece
+            // start (a wave does about once)
+            const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)g.b * a.region, a.region * 4u);
             const uint32_t* pr = prow[pb];
-            const uint32_t last = a.fgrid - 1;
-            // the piece of the wave's first key: the number of piece starts
-            // pr[1..fgrid) at or below it (pr is non-decreasing; pr[0] = 0),
-            // by four ballots over the row instead of a dependent search
-            const uint32_t p0 = S + wq0 * 16u;
+            const uint32_t p0 = g.s0 + w0;
+            uint32_t ln = lane;
+            asm volatile("" : "+v"(ln));
             uint32_t lo = 0;
 #pragma unroll
             for (int m = 0; m < (kMaxFusedGrid + 63) / 64; m++) {
-                const uint32_t k = 1u + lane + 64u * (uint32_t)m;
-                lo += (uint32_t)__builtin_popcountll(__ballot(k < a.fgrid && pr[min(k, (uint32_t)kMaxFusedGrid)] <= p0));
+                const uint32_t k = 1u + ln + 64u * (uint32_t)m;
+                lo += (uint32_t)__builtin_popcountll(
+                    __ballot(k < a.fgrid && pr[min(k, (uint32_t)kMaxFusedGrid)] <= p0));
             }
-            uint32_t cur = rfl(pr[lo]), nxt = rfl(pr[lo + 1]);
-            // common case (no piece boundary and no item end inside the load):
-            // the whole offset but lane*4 is uniform and goes to soffset
-            uint32_t soff[kPartKeysPerThread];
-            const uint32_t end = S + nk;
+            const uint32_t k0 = p0 + ln;
+            uint32_t pl = lo, nl = pr[lo + 1];
+            int32_t t = (int32_t)(nl - k0);
+            uint32_t u = (k0 + lo * a.piece_cap - pr[lo]) * 4u;
+            // lanes whose key (k0 + 64 j) passed the next piece start walk on
+            // (keys past the item, in a segment's last waves, load whatever
+            // their slot holds: count() replaces them)
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++) {
-                const uint32_t pj = p0 + 64u * (uint32_t)j;  // the wave's first key of this load
-                while (lo < last && nxt <= pj) {             // uniform advance
-                    lo++;
-                    cur = nxt;
-                    nxt = rfl(pr[lo + 1]);
-                }
-                if ((lo < last && nxt < pj + 64u) || pj + 64u > end) {  // per-lane walk
-                    const uint32_t pl = pj + lane;
-                    uint32_t k = lo, c = cur, n = nxt;
-                    while (k < last && n <= pl) {
-                        k++;
-                        c = n;
-                        n = pr[k + 1];
+                if (__ballot(t <= 64 * j)) {
+                    const uint32_t k = k0 + 64u * (uint32_t)j;
+                    while (k >= nl && pl + 1 < a.fgrid) {
+                        pl++;
+                        const uint32_t cl = nl;
+                        nl = pr[pl + 1];
+                        t = (int32_t)(nl - k0);
+                        u = (k0 + pl * a.piece_cap - cl) * 4u;
                     }
-                    key[j] = pl < end ? (k * a.piece_cap + (pl - c)) * 4u : kOOB;
-                    soff[j] = 0;
-                } else {
-                    key[j] = lane * 4u;
-                    soff[j] = (lo * a.piece_cap + (pj - cur)) * 4u;
                 }
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, u, 256 * j, kLdAux);
             }
-#pragma unroll
-            for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, key[j], soff[j], kLdAux);
         } else {
-            const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + base, (uint64_t)nk * 4u);
+            const __amdgpu_buffer_rsrc_t src =
+                uniform_rsrc(a.part1 + (uint64_t)g.base8 * kBucketAlign, (uint64_t)g.nk * 4u);
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wq0 * 16u + lane) * 4u, j * 256, kLdAux);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (w0 + lane) * 4u, j * 256, kLdAux);
         }
     };
-    uint32_t nk_next = 0;
-    uint64_t base_next = 0;
+    // count: every key's slice counter (LDS address (key >> 12) & 0x3fc: the
+    // slice and bit 21) gets 2; the returned count is the key's byte offset in
+    // its slice run.  The ranks go to LDS (two u16 per word, [pair][thread]:
+    // conflict-free), the key becomes (counter address << 16) | its low 16
+    // bits, all that scatter() needs of it (in registers with the ranks, the
+    // scan's registers would spill, and a spill reload waits for every key
+    // load in flight).  Slots past the item (the last waves of a segment)
+    // become the dummy key of the item's bucket: bit 21 flipped, slice 0.
+    auto count = [&](const Item& g) {
+        const uint32_t nk = g.nk;
+        if (wave * kWaveSlots + kWaveSlots > nk) {
+            const uint32_t dummy = ((g.b & 1u) ^ 1u) << kL1Shift;
+#pragma unroll
+            for (int j = 0; j < kPartKeysPerThread; j++)
+                key[j] = wave * kWaveSlots + 64u * (uint32_t)j + lane < nk ? key[j] : dummy;
+        }
+#pragma unroll
+        for (int h = 0; h < kPartKeysPerThread; h += 8) {
+            uint32_t r[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t sa = (key[h + j] >> (kSliceBits - 2)) & ((2 * kSubs - 1) << 2);
+                r[j] = atomicAdd(&lcnt[sa >> 2], 2u);
+                key[h + j] = __builtin_amdgcn_perm(sa, key[h + j], 0x05040100u);  // sa.lo16 : key.lo16
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                rnk[(h / 2 + j) * kPartThreads + tid] = r[2 * j] | (r[2 * j + 1] << 16);
+        }
+    };
+    // scatter: each key's u16 to its slice run in the stage, at the run start
+    // (after the scan, loff) + its rank (the dummy slots land in [nk,
+    // kPartChunk)).  Every LDS read of a round is issued before its first use.
+    auto scatter = [&]() {
+        uint8_t* const st8 = (uint8_t*)stage;
+#pragma unroll
+        for (int h = 0; h < kPartKeysPerThread; h += 8) {
+            uint32_t o[8], rk[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                rk[j] = rnk[(h / 2 + j) * kPartThreads + tid];
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                o[j] = *(const uint32_t*)((const uint8_t*)loff + (key[h + j] >> 16));
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                *(uint16_t*)(st8 + o[j] + ((j & 1) ? rk[j / 2] >> 16 : rk[j / 2] & 0xffffu)) = (uint16_t)key[h + j];
+        }
+    };
+
+    Item g{};
     int pb = 0;
-    if (kP2Pipe && blockIdx.x < nitems) {
-        geo(blockIdx.x, nk_next, base_next);
-        stage_pieces(base_next, 0);
-        P2_BARRIER();
-        load(base_next, nk_next, 0);
+    if (blockIdx.x < nitems) {
+        g = geo(blockIdx.x);
+        stage_pieces(g, 0);
+        lds_barrier();
+        load(g, 0);
     }
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
-        uint32_t nk = nk_next;
-        uint64_t base = base_next;
-        if (!kP2Pipe)
-            geo(item, nk, base);
-        if (tid < kSubs)
-            lcnt[tid] = 0;
-        if (!kP2Pipe)
-            stage_pieces(base, 0);
-        P2_BARRIER();
-        if (!kP2Pipe)
-            load(base, nk, 0);
-        // the counting atomic returns each key's rank inside its slice, so the
-        // scatter after the scan is a plain LDS store
-        uint32_t rank[kPartKeysPerThread / 2];  // two u16 ranks per word (rank < kPartChunk)
-#pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++) {
-            // lanes past the chunk are dropped (and their key overwritten: the
-            // build without the overwrite ran 0.78 instead of 0.70 ms at 9000 B,
-            // with 29% more HBM reads by PMC; same load instructions)
-            const bool v = slot(j) < nk;
-            if (!v)
-                key[j] = DQDK_KEY_NONE;
-            const uint32_t r = v ? atomicAdd(&lcnt[(key[j] >> kSliceBits) & (kSubs - 1)], 1u) : 0u;
-            rank[j / 2] = (j & 1) ? (rank[j / 2] | (r << 16)) : r;
+        const uint32_t nk = g.nk;
+        count(g);
+        lds_barrier();
+        // wave 0: run starts (byte offsets in the stage) in counter order from
+        // the item's half (its slices first, then the dummy half), the item's
+        // run offsets; the counts are zeroed for the next item
+        if (wave == 0) {
+            const uint32_t q = (lane + (g.b & 1u) * (kSubs / 4)) & 63u;  // counters 4q .. 4q + 3
+            const u32x4_t c = ((const u32x4_t*)lcnt)[q];
+            ((u32x4_t*)lcnt)[q] = u32x4_t{0u, 0u, 0u, 0u};
+            const uint32_t sum = c.x + c.y + c.z + c.w;
+            const uint32_t ex = wave_incl_scan_dpp(sum) - sum;
+            const u32x4_t o4 = {ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
+            ((u32x4_t*)loff)[q] = o4;
+            uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
+            if (lane < kSubs / 4) {
+                ro[4 * lane] = (uint16_t)(o4.x / 2);
+                ro[4 * lane + 1] = (uint16_t)(o4.y / 2);
+                ro[4 * lane + 2] = (uint16_t)(o4.z / 2);
+                ro[4 * lane + 3] = (uint16_t)(o4.w / 2);
+            } else if (lane == kSubs / 4) {
+                ro[kSubs] = (uint16_t)(ex / 2);
+            }
         }
-        P2_BARRIER();
-        wave0_excl_scan(lcnt, loff, kSubs, false);
-        P2_BARRIER();
-        if (tid <= kSubs)
-            a.runs[(uint64_t)item * kItemOffs + tid] = (uint16_t)loff[tid];
-#pragma unroll
-        for (int j = 0; j < kPartKeysPerThread; j++)
-            if (slot(j) < nk)
-                stage[loff[(key[j] >> kSliceBits) & (kSubs - 1)] + ((rank[j / 2] >> (16 * (j & 1))) & 0xffffu)] =
-                    (uint16_t)(key[j] & ((1u << kSliceBits) - 1));
+        lds_barrier();
+        scatter();
         // the next item's keys load while this one is written out
-        const bool more = kP2Pipe && item + gridDim.x < nitems;
+        const bool more = item + gridDim.x < nitems;
         if (more) {
-            geo(item + gridDim.x, nk_next, base_next);
-            stage_pieces(base_next, pb ^ 1);
+            g = geo(item + gridDim.x);
+            stage_pieces(g, pb ^ 1);
         }
-        P2_BARRIER();
+        lds_barrier();
         if (more)
-            load(base_next, nk_next, pb ^ 1);
-        // 16-B stores: bucket starts are multiples of kBucketAlign keys, and the
-        // stale LDS past nk lands in the bucket's padding (never read)
+            load(g, pb ^ 1);
+        // item i's keys go to part2 [i * kPartChunk, + nk) in 16-B stores
+        // (the dummy keys of the last group are never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;
-#if DQDK_P2ST_AUX
-        // cache policy of the output stores (16 = sc1, write-through: nothing
-        // left dirty in L2 for the kernel-end write-back)
-        const __amdgpu_buffer_rsrc_t drs = uniform_rsrc(a.part2 + base, ((uint64_t)nk + 7u) / 8u * 16u);
-        for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, st4[p]), drs, p * 16u, 0, DQDK_P2ST_AUX);
-#else
-        u32x4_t* dst4 = (u32x4_t*)(a.part2 + base);
+        u32x4_t* dst4 = (u32x4_t*)(a.part2 + (uint64_t)item * kPartChunk);
         for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
             dst4[p] = st4[p];
-#endif
-        P2_BARRIER();
+        // (no barrier here: the stage is rewritten only after the next item's
+        // first two barriers)
     }
 }
 
@@ -1820,11 +1826,13 @@ template __global__ void rx_part2_kernel<2>(HistoArgs);
 // (skewed spectra, hot bins) is appended to a list and redone by the u32
 // form (64 KB LDS) in a second launch over that list.
 struct SliceLds {
-    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads], s_base[kSliceThreads];
+    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads], s_base[kSliceThreads];  // run [lo, hi) of item s_base
     uint8_t s_k[kSliceThreads];
     uint32_t b_i0[kSliceMaxSlots], b_n[kSliceMaxSlots];  // the bucket's first item / items per staged batch
     uint32_t total;
 };
+
+constexpr uint32_t kSliceMask = (1u << kSliceBits) - 1;
 
 template <bool kPacked>
 __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
@@ -1898,7 +1906,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             const uint32_t lo = ro[0], hi = ro[1];
             sl.s_lo[tid] = lo;
             sl.s_hi[tid] = hi;
-            sl.s_base[tid] = sc(k)[kOffItems + 2 * it];  // in kBucketAlign keys
+            sl.s_base[tid] = it;
             sl.s_k[tid] = (uint8_t)k;
             mine = hi - lo;
         }
@@ -1922,7 +1930,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         return;  // no events for this slice: table untouched
     if (kPacked && total > 0xffffu) {  // a u16 bin could overflow: the u32 form redoes it
         if (tid == 0)
-            a.scratch[a.heavy_off + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
+            a.scratch[kOffHeavyList + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
         return;
     }
     const uint64_t sb = (uint64_t)s << kSliceBits;
@@ -1965,7 +1973,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         };
         // a buffer descriptor per item whose extent ends at the run's last
         // dword (so the loads need no per-lane bound); items start at
-        // multiples of kBucketAlign keys: dword-aligned
+        // multiples of kPartChunk keys: dword-aligned
         auto issue = [&](uint32_t j, uint32_t p0, uint32_t (&w)[kNI][kKG]) -> uint32_t {
             uint32_t steps = 0;
 #pragma unroll
@@ -1976,7 +1984,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 const uint32_t jc = jj < nit ? jj : 0u;
                 const uint32_t dlo = klo >> 1, dhi = (khi + 1) >> 1;
                 const uint16_t* base = a.part2 + (uint64_t)rfl(sl.s_k[jc]) * a.part2_stride +
-                                       (uint64_t)rfl(sl.s_base[jc]) * kBucketAlign;
+                                       (uint64_t)rfl(sl.s_base[jc]) * kPartChunk;
                 const __amdgpu_buffer_rsrc_t src = uniform_rsrc(base, (uint64_t)dhi * 4u);
 #pragma unroll
                 for (int g = 0; g < kKG; g++)
@@ -1994,10 +2002,11 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
 #pragma unroll
                 for (int g = 0; g < kKG; g++) {
                     const uint32_t k0 = 2 * (dlo + p0 + 64 * g + lane);  // key index of the low half
+                    // (part2 stores a key's low 16 bits: bits 14-15 are its slice's)
                     if (k0 >= klo && k0 < khi)
-                        slice_count<kPacked>(h, w[q][g] & 0xffffu);
+                        slice_count<kPacked>(h, w[q][g] & kSliceMask);
                     if (k0 + 1 >= klo && k0 + 1 < khi)
-                        slice_count<kPacked>(h, w[q][g] >> 16);
+                        slice_count<kPacked>(h, (w[q][g] >> 16) & kSliceMask);
                 }
             }
         };
@@ -2069,7 +2078,7 @@ __global__ void __launch_bounds__(kSliceThreads) rx_slice_heavy_kernel(HistoArgs
     __shared__ SliceLds sl;
     const uint32_t n = a.scratch[kOffHeavyN];
     for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-        slice_histo<false>(a, a.scratch[a.heavy_off + k], h, sl);
+        slice_histo<false>(a, a.scratch[kOffHeavyList + k], h, sl);
         __syncthreads();
     }
 }

@@ -230,7 +230,8 @@ class RxQueue:
         cnt = (C.c_uint64 * ns)()
         L.check(L.lib().dqdk_gpu_timing_read(self._h, ms, cnt, ns), "timing_read")
         names = [L.lib().dqdk_gpu_timing_stage_name(k) for k in range(ns)]
-        return {nm.decode(): {"ms": ms[k], "launches": int(cnt[k])} for k, nm in enumerate(names) if nm}
+        return {nm.decode(): {"ms": ms[k], "launches": int(cnt[k])} for k, nm in enumerate(names)
+                if nm and not nm.startswith(b"(")}  # "(unused)" stage slots
 
 
 def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, directory: str = "") -> str:

@@ -95,7 +95,7 @@ def test_fused_full_size_vs_oracle(n, L, stride, payloadsz, faulty):
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     assert_same(res, cnt, table, ores, ocnt, otable)
     if faulty:
-        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 1000  # rx_fixup takes these back
+        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 1000  # rx_part1's fixup takes these back
         assert ocnt["oob_events"] > 0
     else:
         assert (ores["status"] == D.RX_OK).all()

@@ -368,7 +368,7 @@ def test_configs2_jumbo_full_batch_vs_oracle():
 
 @pytest.mark.parametrize("hpath,kernels", [
     (D.F_HISTO_ATOMIC, {"rx_decode", "rx_abort", "rx_count", "rx_histo_atomic"}),
-    (D.F_HISTO_PARTITIONED | D.F_HISTO_EAGER, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_hist_prep", "rx_part2",
+    (D.F_HISTO_PARTITIONED | D.F_HISTO_EAGER, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_part2",
                              "rx_slice_histo", "rx_slice_heavy"})], ids=["atomic", "partitioned"])
 def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels):
     _need_gpu()
