@@ -166,6 +166,7 @@ struct dqdk_gpu_queue {
     uint32_t max_batch = 0;
     int histo = 0;
     int cu_count = 256;
+    int dec_cus = 256;             // fused decode blocks at most (DQDK_GPU_DECODE_CUS, default all CUs)
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     hipEvent_t switch_ev = nullptr;  // orders a stream switch after the old stream's work
@@ -371,7 +372,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     // Not when the caller wants those records, nor under batch-abort
     // accounting (the frames after the first failure are known only after
     // the decode; the records path counts exactly the accounted frames).
-    const FusedGeom fg = fused_geom(n, q->E, (uint64_t)q->cu_count);
+    const FusedGeom fg = fused_geom(n, q->E, (uint64_t)q->dec_cus);
     const bool fused = partitioned && !d_keys && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT) && q->d_fix &&
                        !(q->cfg.flags & DQDK_GPU_F_HISTO_UNFUSED) &&
                        (uint64_t)kL1Buckets * fg.region <= q->fused_elems;
@@ -690,6 +691,9 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                (cfg->mode == DQDK_MODE_LISTWAVE || cfg->mode == DQDK_MODE_LISTMODE ||
                 cfg->mode == DQDK_MODE_ENERGYHISTO);  // is_store_histo, src/tristan.c:65-70
     q->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    q->dec_cus = q->cu_count;
+    if (const char* v = getenv("DQDK_GPU_DECODE_CUS"))
+        q->dec_cus = std::max(1, std::min(q->cu_count, atoi(v)));
     q->alloc_kind = internal_alloc_kind(q->E);
     if (const char* rs = getenv("DQDK_GPU_RAW_SYNC"))
         q->raw_sync = atoi(rs) != 0;
@@ -743,7 +747,7 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                                   1, std::min({kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1),
                                                kHistStageBytes / slot_bytes}));
             // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
-            const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->cu_count);
+            const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->dec_cus);
             const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
             q->ovf_blk_elems = fg.grid * ((nsuper + fg.grid - 1) / fg.grid) * (64 * kFWaves) * q->E;
             // part1 holds the fused decode's pieces, then rx_part1's region
