@@ -264,7 +264,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
             qr.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
                               d_keys.data_ptr())
             torch.cuda.synchronize(dev)
-    items = K // (1 << 14) + 284 + 1  # part2 work items (16K-key chunks of the 284 buckets)
+    items = K // 15360 + 284 + 1  # part2 work items (15360-key chunks of the 284 buckets)
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
     if histo and E:
@@ -272,7 +272,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         touched = int(torch.unique(kk[kk >= 0] >> 14).numel())  # 16K-bin slices with >= 1 event
     alg = {
         # the metric's path: desc + frame (the UDP checksum reads all of it) + result + 4-B record per event
-        # (no records and no histogram: parse + checksum only, configs[1] -- nothing written per event)
+        # (the fused decode writes 8-B key triples, 2.67 B per event, so this over-counts
+        # its writes) (no records and no histogram: parse + checksum only, configs[1] -- nothing written)
         "rx_decode": n * (16 + 8) + frame_bytes + (4 * K if keys_written else 0),
         "rx_abort": 8 * n,
         "rx_count": 8 * n,
@@ -282,7 +283,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         # fused path: the per-bucket scans of the decode's piece sizes (checksum-failed
         # frames taken back and overflow keys grouped: none in the timed workload)
         "rx_fixup": 284 * 256 * 4 + 284 * 257 * 4,
-        "rx_part2": 6 * K + runs,
+        # fused path: key triples read (8 B per 3 keys) + u16 keys written; records path: u32 keys read
+        "rx_part2": (4 * K if pass_records else K * 8 // 3) + 2 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
         # (per batch: one slice pass sweeps for hist_k staged batches)

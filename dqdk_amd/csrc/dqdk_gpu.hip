@@ -386,6 +386,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.scratch = slot_scratch;
         ra.part1 = q->d_part1;
         ra.piece_cap = fg.cap;
+        ra.piece_words = fg.words;
         ra.region = fg.region;
         ra.ovf = q->d_keys;
         ra.fix = q->d_fix;
@@ -457,6 +458,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             ha.fused = 1;
             ha.fgrid = fg.grid;
             ha.piece_cap = fg.cap;
+            ha.piece_words = fg.words;
             ha.region = fg.region;
         }
         if (!partitioned) {

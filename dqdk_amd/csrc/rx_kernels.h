@@ -53,8 +53,9 @@ constexpr int kSliceBits = 14;                              // 2^14 bins per sli
 constexpr int kSubs = 1 << (kL1Shift - kSliceBits);         // 128 slices per bucket
 constexpr int kSlices = kL1Buckets * kSubs;                 // 36352 (36288 used)
 constexpr int kPartThreads = 1024;                          // part1/part2 block size
-constexpr int kPartKeysPerThread = 16;
-constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 16384 keys staged in LDS
+constexpr int kPartKeysPerThread = 15;                      // five key triples per lane
+constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 15360 key slots staged in LDS (an item)
+constexpr int kPartTriples = kPartChunk / 3;                // 5120 triples: a gathered item
 constexpr int kSliceThreads = 512;
 constexpr int kSliceMaxSlots = 16;  // staged batches one slice pass can take
 #ifndef DQDK_P1_KEYS
@@ -83,35 +84,48 @@ constexpr int kMaxFusedGrid = 256;  // fused decode blocks (one per CU)
 constexpr int kOffOff1 = kZeroWords;  // [kL1Buckets + 1] bucket starts of rx_part1's output (prep)
 constexpr int kOffIstart = kOffOff1 + 288;  // [kL1Buckets + 1] first part2 item of each bucket; [284] = items (rx_part2)
 // fused path: keys of each (bucket, block) piece [kL1Buckets][kMaxFusedGrid] (decode),
-// and their exclusive scans per bucket [kL1Buckets][kMaxFusedGrid + 1] (prep)
+// and per bucket the exclusive scans of its pieces' keys and of their key
+// triples [kL1Buckets][kMaxFusedGrid + 1] each (rx_part1's prologue)
 constexpr int kOffPieceN = kOffIstart + 288;
 constexpr int kOffPiecePre = kOffPieceN + kL1Buckets * kMaxFusedGrid;
-constexpr int kOffEnd = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);
+constexpr int kOffPiecePreT = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);
+constexpr int kOffEnd = kOffPiecePreT + kL1Buckets * (kMaxFusedGrid + 1);
 constexpr int kSegsPerBucket = 2;  // fused: the bucket's pieces (one gathered sequence), then rx_part1's overflow run
-// items of a batch of nk keys: one per started 16K-key chunk of each segment
-__host__ __device__ constexpr uint64_t max_items(uint64_t nk) { return nk / 16384 + (uint64_t)kL1Buckets * kSegsPerBucket + 1; }
+// items of a batch of nk keys: one per started chunk of each segment (a
+// bucket's gathered triples number at most its keys / 3 + one per piece)
+__host__ __device__ constexpr uint64_t max_items(uint64_t nk)
+{
+    return nk / kPartChunk + (uint64_t)kL1Buckets * (kSegsPerBucket + 1) + 1;
+}
 constexpr int kOffHeavyList = kOffEnd;  // [kSlices] (slot 0 of a slice pass) slices redone in u32
 // u32 words of one staged slot's scratch
 constexpr uint64_t kHistScratchWords = kOffHeavyList + kSlices;
-constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one 16K-key chunk of a segment)
+constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one chunk of a segment)
 
 // Fused decode (rx_decode_fused): 1024-thread blocks, one per CU, persistent.
 // Keys of a round are counted into an LDS stage per L1 bucket (kFCap keys
 // each), then appended to the block's piece of that bucket (a private
-// region: no device atomics).  The fused region is [bucket][block][cap]: a
+// region: no device atomics) as key triples: three 21-bit bucket-local keys
+// per 8 bytes (k0 | k1 << 21 | k2 << 42; 2.67 B a key).  A round flushes
+// whole triples (whole 128-B lines of 48 keys in the lines policy) and
+// carries the rest; the last flush pads a piece's last triple, whose valid
+// keys the piece size tells.  The fused region is [bucket][block][cap]: a
 // bucket's pieces are adjacent, in block order.  Keys past kFCap in a round,
-// or past a full piece, go to the block's overflow region, which rx_part1
-// groups afterwards.
+// or past a full piece, go to the block's overflow region (u32 keys), which
+// rx_part1 groups afterwards.
 constexpr int kFWaves = 16;
 constexpr int kFThreads = kFWaves * 64;
 #ifndef DQDK_FCAP
 #define DQDK_FCAP 112
 #endif
 constexpr int kFCap = DQDK_FCAP;
+constexpr uint32_t kTripleMask = (1u << kL1Shift) - 1;  // a bucket-local key
+constexpr uint32_t kLineKeys = 48;                     // keys of one 128-B line of triples
 struct FusedGeom {
     uint32_t grid;    // decode blocks
-    uint32_t cap;     // keys per piece: 1.25x the block's uniform share + slack, whole 128-B lines
-    uint64_t region;  // keys per bucket: grid pieces + 32 (part2's 16-B store tail)
+    uint32_t cap;     // keys per piece: 1.25x the block's uniform share + slack, whole 128-B lines of triples
+    uint32_t words;   // u32 words per piece (cap * 2 / 3)
+    uint64_t region;  // u32 words per bucket: grid pieces + 32
 };
 __host__ __device__ constexpr FusedGeom fused_geom(uint64_t n, uint64_t E, uint64_t cus)
 {
@@ -119,8 +133,9 @@ __host__ __device__ constexpr FusedGeom fused_geom(uint64_t n, uint64_t E, uint6
     const uint64_t g0 = nsuper < cus ? nsuper : cus;
     const uint64_t grid = g0 < (uint64_t)kMaxFusedGrid ? (g0 ? g0 : 1) : (uint64_t)kMaxFusedGrid;
     const uint64_t spt = (nsuper + grid - 1) / grid;
-    const uint64_t cap = ((spt * kFThreads * E * 5 / 4) / kL1Buckets + 64 + 31) & ~31ull;
-    return FusedGeom{(uint32_t)grid, (uint32_t)cap, grid * cap + 32};
+    const uint64_t cap = ((spt * kFThreads * E * 5 / 4) / kL1Buckets + 64 + kLineKeys - 1) / kLineKeys * kLineKeys;
+    const uint64_t words = cap / 3 * 2;
+    return FusedGeom{(uint32_t)grid, (uint32_t)cap, (uint32_t)words, grid * words + 32};
 }
 // part1/part2 elements: the fused pieces, then rx_part1's output region
 __host__ __device__ constexpr uint64_t part_elems(uint64_t nk, uint64_t fused_elems)
@@ -143,9 +158,10 @@ struct RxArgs {
     uint32_t* cnt1;           // partitioned histogram: bucket counts (+ KEY_NONE records for non-OK frames), or null
     // fused path (rx_decode_fused) only:
     uint32_t* scratch;        // the slot's histogram scratch (piece sizes, overflow / fixup counts)
-    uint32_t* part1;          // pieces [bucket][block] of piece_cap keys
+    uint32_t* part1;          // pieces [bucket][block] of piece_cap keys (piece_words u32 words of triples)
     uint32_t piece_cap;
-    uint64_t region;          // keys per bucket (fused_geom)
+    uint32_t piece_words;
+    uint64_t region;          // u32 words per bucket (fused_geom)
     uint32_t* ovf;            // overflow list (n*E keys)
     uint32_t* ovf_blk;        // per-block private overflow regions (gridDim.x * ovf_blk_cap keys)
     uint32_t ovf_blk_cap;
@@ -182,6 +198,7 @@ struct HistoArgs {
     uint32_t fused;     // the keys are the fused decode's pieces + rx_part1's run of its overflow
     uint32_t fgrid;     // fused: decode blocks (pieces per bucket)
     uint32_t piece_cap;
+    uint32_t piece_words;
     uint64_t region;
     // the slice pass runs over nslots staged batches: batch k's scratch,
     // part2 keys and run offsets sit k strides (elements) after the first

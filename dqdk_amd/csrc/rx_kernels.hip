@@ -788,7 +788,7 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 // Frames decoded but later failing the UDP checksum are listed for rx_fixup.
 // ===========================================================================
 struct FusedLds {
-    uint32_t stage[kL1Buckets * kFCap + 64];  // (+64: the flush reads 128 slots per bucket)
+    uint32_t stage[kL1Buckets * kFCap + 96];  // (+96: the flush reads 192 slots per bucket; the lanes' sink words)
     uint32_t scnt[kL1Buckets + 4];   // staged keys per bucket this round (returning LDS atomics)
     uint32_t sum[kFWaves * 64];      // checksum word sums per frame
     uint32_t oob[kFWaves * 64];      // out-of-bounds events per frame
@@ -926,12 +926,16 @@ __device__ __forceinline__ void fused_pair(const u32x4& va, const u32x4& vb, uin
     }
 }
 
-// Append the round's staged runs to the block's pieces.  Wave w owns buckets
-// w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece cursor `cur`).
-// All LDS reads of a few buckets are issued before their stores, and every
-// store is issued (its offset dropped past the run): no dependent chain per
-// bucket and a fixed VMEM pattern.  Rare: keys past a full piece go to the
-// block's overflow region (slot from an LDS counter).
+// Append the round's staged runs to the block's pieces as key triples.  Wave
+// w owns buckets w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece
+// cursor `cur`, in keys).  A round flushes whole triples (lines policy: whole
+// 128-B lines of 48 keys) and carries the rest to the next round; the last
+// flush writes everything, its last triple padded (the piece size marks the
+// valid keys).  All LDS reads of a few buckets are issued before their
+// stores, and every store is issued (its offset dropped past the run): no
+// dependent chain per bucket and a fixed VMEM pattern.  Rare: keys past a
+// full piece go to the block's overflow region (u32 keys, slot from an LDS
+// counter).
 template <bool kLines>
 __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int lane, uint32_t wave, uint32_t& cur,
                                             __amdgpu_buffer_rsrc_t ovf_rsrc, bool last)
@@ -940,10 +944,13 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
     uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
         c = min(lds.scnt[b] / kCntUnit, (uint32_t)kFCap);
-        // lines mode: whole 128-B lines only (the piece cursor stays line-
-        // aligned, so no store writes part of a line); the rest is carried
-        w = kLines && !last ? (c & ~31u) : c;
-        fit = min(w, a.piece_cap - cur);
+        // lines policy: whole 128-B lines of triples (the piece cursor stays
+        // line-aligned, so no store writes part of a line); else whole triples
+#ifndef DQDK_FLUSH_UNIT
+#define DQDK_FLUSH_UNIT kLineKeys
+#endif
+        w = last ? c : kLines ? c - c % (uint32_t)(DQDK_FLUSH_UNIT) : c - c % 3u;
+        fit = min(w, a.piece_cap - cur);  // (cap and cur are multiples of 3: so is fit before the last flush)
     }
     const uint32_t base = cur;
     cur += fit;
@@ -952,15 +959,16 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
 #define DQDK_FLUSH_G 6
 #endif
     constexpr int G = DQDK_FLUSH_G;  // buckets per batch of reads (VGPRs: the load ring stays live)
-    uint32_t* const piece0 = a.part1 + (uint64_t)blockIdx.x * a.piece_cap;
+    uint32_t* const piece0 = a.part1 + (uint64_t)blockIdx.x * a.piece_words;
 #pragma unroll 1
     for (int h = 0; h < (NJ + G - 1) / G; h++) {
-        uint32_t v0[G], v1[G];
+        uint32_t v[G][3];
 #pragma unroll
         for (int q = 0; q < G; q++) {
             const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(h * G + q), (uint32_t)kL1Buckets - 1);
-            v0[q] = lds.stage[bj * kFCap + lane];
-            v1[q] = lds.stage[bj * kFCap + 64 + lane];
+#pragma unroll
+            for (int i = 0; i < 3; i++)  // (lanes past the run read the next bucket's stage or the sink: unused)
+                v[q][i] = lds.stage[bj * kFCap + 3 * lane + i];
         }
 #pragma unroll
         for (int q = 0; q < G; q++) {
@@ -969,14 +977,17 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
                 const uint32_t bj = wave + (uint32_t)kFWaves * (uint32_t)j;
                 const uint32_t fj = rdl(fit, j), bsj = rdl(base, j);
                 const __amdgpu_buffer_rsrc_t prs =
-                    uniform_rsrc(piece0 + (uint64_t)min(bj, (uint32_t)kL1Buckets - 1) * a.region, a.piece_cap * 4u);
-                const uint32_t o = (bsj + (uint32_t)lane) * 4u;
+                    uniform_rsrc(piece0 + (uint64_t)min(bj, (uint32_t)kL1Buckets - 1) * a.region, a.piece_words * 4u);
+                // the last flush's last triple: its slots past the run hold 0
+                const uint32_t k0 = v[q][0] & kTripleMask;
+                const uint32_t k1 = 3u * lane + 1u < fj ? v[q][1] & kTripleMask : 0u;
+                const uint32_t k2 = 3u * lane + 2u < fj ? v[q][2] & kTripleMask : 0u;
+                const u32x2 t = {k0 | (k1 << kL1Shift), (k1 >> (32 - kL1Shift)) | (k2 << (2 * kL1Shift - 32))};
+                const uint32_t o = (bsj / 3u + (uint32_t)lane) * 8u;
 #ifndef DQDK_DIAG_FNOSTORE  // timing diagnostic only: the flush without its stores
-                __builtin_amdgcn_raw_buffer_store_b32(v0[q], prs, (uint32_t)lane < fj ? o : kOOB, 0, DQDK_FST_AUX);
-                __builtin_amdgcn_raw_buffer_store_b32(v1[q], prs, (uint32_t)lane + 64u < fj ? o + 256u : kOOB, 0,
-                                                      DQDK_FST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b64(t, prs, 3u * lane < fj ? o : kOOB, 0, DQDK_FST_AUX);
 #else
-                asm volatile("" ::"v"(v0[q]), "v"(v1[q]), "v"(o), "s"(fj));
+                asm volatile("" ::"v"(t.x), "v"(t.y), "v"(o), "s"(fj));
 #endif
             }
         }
@@ -992,16 +1003,24 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
         for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
             __builtin_amdgcn_raw_buffer_store_b32(lds.stage[bj * kFCap + fj + t], ovf_rsrc, 4u * (o + t), 0, 0);
     }
-    // carry the remainders (< 32 keys, so source and destination do not overlap)
-    for (uint64_t m = kLines ? __ballot(w != 0 && c > w) : 0ull; m; m &= m - 1) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        const uint32_t bj = wave + (uint32_t)kFWaves * j;
-        const uint32_t wj = rdl(w, j), r = rdl(c, j) - wj;
-        uint32_t x = 0;
-        if ((uint32_t)lane < r)
-            x = lds.stage[bj * kFCap + wj + lane];
-        if ((uint32_t)lane < r)
-            lds.stage[bj * kFCap + lane] = x;
+    // carry the remainders to the stage's start (fewer keys than were
+    // flushed, so source and destination do not overlap)
+    if (kLines) {  // up to 47 keys: a wave per bucket
+        for (uint64_t m = __ballot(w != 0 && c > w); m; m &= m - 1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            const uint32_t bj = wave + (uint32_t)kFWaves * j;
+            const uint32_t wj = rdl(w, j), r = rdl(c, j) - wj;
+            uint32_t x = 0;
+            if ((uint32_t)lane < r)
+                x = lds.stage[bj * kFCap + wj + lane];
+            if ((uint32_t)lane < r)
+                lds.stage[bj * kFCap + lane] = x;
+        }
+    } else if (w != 0 && c > w) {  // up to 2 keys: each lane its own bucket
+        const uint32_t x0 = lds.stage[b * kFCap + w], x1 = lds.stage[b * kFCap + w + 1];
+        lds.stage[b * kFCap] = x0;
+        if (c - w > 1)
+            lds.stage[b * kFCap + 1] = x1;
     }
     if (b < (uint32_t)kL1Buckets)
         lds.scnt[b] = (c - w) * kCntUnit;
@@ -1200,35 +1219,37 @@ __device__ __forceinline__ void fused_fixup(const RxArgs& a, const HistoArgs& h,
 {
     const uint32_t nfix = a.scratch[kOffFixN];
     const int lane = threadIdx.x & 63;
-    // first, one wave per bucket: the exclusive scan of its piece sizes
-    // (rx_part2's segment sizes and piece starts)
+    // first, one wave per bucket: the exclusive scans of its pieces' keys and
+    // key triples (rx_part2's segment sizes, piece starts and valid keys)
     for (uint32_t b = gw; b < (uint32_t)kL1Buckets; b += nw) {
         const uint32_t* cn = a.scratch + kOffPieceN + b * kMaxFusedGrid;
         uint32_t* pre = a.scratch + kOffPiecePre + b * (kMaxFusedGrid + 1);
-        uint32_t v[4], sum = 0;
+        uint32_t* preT = a.scratch + kOffPiecePreT + b * (kMaxFusedGrid + 1);
+        uint32_t v[4], vt[4], sum = 0, sumt = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t blk = (uint32_t)lane * 4u + i;
             v[i] = blk < h.fgrid ? cn[blk] : 0u;
+            vt[i] = (v[i] + 2u) / 3u;
             sum += v[i];
+            sumt += vt[i];
         }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t x = __shfl_up(incl, o);
-            if (lane >= o)
-                incl += x;
-        }
-        uint32_t run = incl - sum;
+        const uint32_t incl = wave_incl_scan_dpp(sum), inclt = wave_incl_scan_dpp(sumt);
+        uint32_t run = incl - sum, runt = inclt - sumt;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t blk = (uint32_t)lane * 4u + i;
-            if (blk < h.fgrid)
+            if (blk < h.fgrid) {
                 pre[blk] = run;
+                preT[blk] = runt;
+            }
             run += v[i];
+            runt += vt[i];
         }
-        if (lane == 63)
+        if (lane == 63) {
             pre[h.fgrid] = incl;
+            preT[h.fgrid] = inclt;
+        }
     }
     for (uint32_t k = gw; k < nfix; k += nw) {
         const uint32_t i = a.fix[k];
@@ -1567,24 +1588,27 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 {
     constexpr int kMaxSeg = kL1Buckets * kSegsPerBucket;
     constexpr int kPWaves = kPartThreads / 64;
-    constexpr uint32_t kWaveSlots = (uint32_t)kPartChunk / kPWaves;  // 1024 key slots per wave
+    constexpr int kJT = kPartKeysPerThread / 3;                      // triple loads per lane (gathered items)
+    constexpr uint32_t kWaveKeys = (uint32_t)kPartChunk / kPWaves;     // 960 key slots per wave
+    constexpr uint32_t kWaveTriples = kWaveKeys / 3;                  // 320 triple slots per wave
+    constexpr uint32_t kDummy = 1u << kL1Shift;  // a slot past the item or a triple's pad: counter 128
+    constexpr int kRankWords = (kPartKeysPerThread + 1) / 2;
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
-    // counters / run starts of 2 * kSubs slices: bit 21 of a key (the bucket's
-    // low bit) is part of its counter index, so the item's slices use one half
-    // and the other half holds the dummy slice of the slots past the item
+    // counters / run starts: [0, 128) the slices, 128 the dummy slice
     __shared__ __attribute__((aligned(16))) uint32_t lcnt[2 * kSubs];
     __shared__ __attribute__((aligned(16))) uint32_t loff[2 * kSubs];
-    __shared__ uint32_t rnk[kPartKeysPerThread / 2 * kPartThreads];  // count() -> scatter()
-    __shared__ uint32_t prow[2][kMaxFusedGrid + 1];
+    __shared__ uint32_t rnk[kRankWords * kPartThreads];  // count() -> scatter()
+    __shared__ uint32_t prt[2][kMaxFusedGrid + 1], prk[2][kMaxFusedGrid + 1];  // piece starts: triples, keys
     __shared__ uint32_t s_cnt[kMaxSeg], s_base8[kMaxSeg], ist[kMaxSeg + 1];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t wsum[kPWaves];
+    __shared__ uint32_t s_nv;  // valid keys of the current item
     const int tid = threadIdx.x;
     const uint32_t lane = (uint32_t)tid & 63u, wave = rfl((uint32_t)tid >> 6);
     const bool fused = a.fused != 0;
     const uint32_t nseg = fused ? (uint32_t)kMaxSeg : (uint32_t)kL1Buckets;
 
-    // ---- prologue: segments (key count, part2 index) and their first items ----
+    // ---- prologue: segments (size, input index) and their first items ----
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
     if (tid < 2 * kSubs)
         lcnt[tid] = 0;
@@ -1592,18 +1616,19 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     uint32_t nit = 0;
     if ((uint32_t)tid < nseg) {
         const uint32_t b = fused ? (uint32_t)tid >> 1 : (uint32_t)tid;
-        uint32_t c;
-        uint64_t base;
-        if (!fused || (tid & 1)) {  // rx_part1's run of the bucket
+        uint32_t c, per;
+        uint64_t base = 0;
+        if (!fused || (tid & 1)) {  // rx_part1's run of the bucket: keys
             c = a.scratch[kOffCur1 + b];
             base = a.part1_base + off1[b];
-        } else {                    // the bucket's pieces
-            c = a.scratch[kOffPiecePre + b * (kMaxFusedGrid + 1) + a.fgrid];
-            base = (uint64_t)b * a.region;
+            per = kPartChunk;
+        } else {                    // the bucket's pieces: key triples
+            c = a.scratch[kOffPiecePreT + b * (kMaxFusedGrid + 1) + a.fgrid];
+            per = kPartTriples;
         }
         s_cnt[tid] = c;
         s_base8[tid] = (uint32_t)(base / kBucketAlign);
-        nit = (c + kPartChunk - 1) / kPartChunk;
+        nit = (c + per - 1) / per;
     }
     const uint32_t incl = wave_incl_scan_dpp(nit);
     if (lane == 63)
@@ -1622,10 +1647,10 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     // ---- an item's geometry (wave-uniform): its segment is the number of
     // segment starts ist[1..nseg) at or below it (nine ballots) ----
     struct Item {
-        uint32_t s0;     // first key of the item in its segment
-        uint32_t nk;     // keys
+        uint32_t s0;     // first unit of the item in its segment (gathered: triples, else keys)
+        uint32_t nu;     // units
         uint32_t b;      // bucket
-        uint32_t base8;  // part2 index / kBucketAlign
+        uint32_t base8;  // contiguous input index / kBucketAlign
         bool gath;       // fused pieces (else one contiguous run)
     };
     // (the lane-derived addresses are opaque to the compiler: hoisted out of
@@ -1640,33 +1665,42 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             t += (uint32_t)__builtin_popcountll(__ballot(k < nseg && ist[min(k, (uint32_t)kMaxSeg)] <= item));
         }
         Item g;
-        g.s0 = (item - rfl(ist[t])) * (uint32_t)kPartChunk;
-        g.nk = min(rfl(s_cnt[t]) - g.s0, (uint32_t)kPartChunk);
-        g.b = fused ? t >> 1 : t;
         g.gath = fused && !(t & 1u);
+        const uint32_t per = g.gath ? (uint32_t)kPartTriples : (uint32_t)kPartChunk;
+        g.s0 = (item - rfl(ist[t])) * per;
+        g.nu = min(rfl(s_cnt[t]) - g.s0, per);
+        g.b = fused ? t >> 1 : t;
         g.base8 = rfl(s_base8[t]) + g.s0 / kBucketAlign;
         return g;
     };
     // a gathered item: its bucket's piece starts (then a barrier)
     auto stage_pieces = [&](const Item& g, int pb) {
-        if (g.gath && (uint32_t)tid <= a.fgrid)
-            prow[pb][tid] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + tid];
+        if (g.gath && (uint32_t)tid <= a.fgrid) {
+            prt[pb][tid] = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + tid];
+            prk[pb][tid] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + tid];
+        }
     };
-    // key slots: wave w takes the item's slots [1024w, 1024w + 1024), 64 per
-    // load (slot(j) = 1024w + 64j + lane)
+    // slots: gathered items, wave w takes the item's triples [320w, 320w +
+    // 320), 64 per load (load j: triple 320w + 64j + lane -> keys 3j .. 3j + 2
+    // of the lane); contiguous items, keys [960w, 960w + 960), 64 per load
+    // (a gathered item's triple j loads into key[2j], key[2j + 1] and is
+    // unpacked in place, from the last triple down)
     uint32_t key[kPartKeysPerThread];
+    uint32_t pad = 0;  // gathered: bit 2j + i set = key 3j + 2 - i is a pad of its piece's last triple
     auto load = [&](const Item& g, int pb) {
-        const uint32_t w0 = wave * kWaveSlots;
+        pad = 0;
         if (g.gath) {
-            // key k of the bucket's sequence lies in piece p (pr[p] <= k <
-            // pr[p + 1]) at region slot p * cap + k - pr[p].  Lane state: t =
-            // start of the next piece - the lane's first key, u = byte offset
-            // of that key were it in the lane's current piece (a load's offset
-            // is u + 256 j); the state moves only where a load crosses a piece
-            // start (a wave does about once)
+            // triple q of bucket b's sequence lies in piece p (prt[p] <= q <
+            // prt[p + 1]) at byte p * words * 4 + (q - prt[p]) * 8 of the
+            // bucket's region.  Lane state: t = start of the next piece - the
+            // lane's first triple, u = byte offset of that triple were it in
+            // the lane's current piece (a load's offset is u + 512 j); the
+            // state moves only where a load reaches a piece's last triple (a
+            // wave does about once)
             const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)g.b * a.region, a.region * 4u);
-            const uint32_t* pr = prow[pb];
-            const uint32_t p0 = g.s0 + w0;
+            const uint32_t* pt = prt[pb];
+            const uint32_t* pk = prk[pb];
+            const uint32_t q0w = g.s0 + wave * kWaveTriples;
             uint32_t ln = lane;
             asm volatile("" : "+v"(ln));
             uint32_t lo = 0;
@@ -1674,70 +1708,101 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             for (int m = 0; m < (kMaxFusedGrid + 63) / 64; m++) {
                 const uint32_t k = 1u + ln + 64u * (uint32_t)m;
                 lo += (uint32_t)__builtin_popcountll(
-                    __ballot(k < a.fgrid && pr[min(k, (uint32_t)kMaxFusedGrid)] <= p0));
+                    __ballot(k < a.fgrid && pt[min(k, (uint32_t)kMaxFusedGrid)] <= q0w));
             }
-            const uint32_t k0 = p0 + ln;
-            uint32_t pl = lo, nl = pr[lo + 1];
-            int32_t t = (int32_t)(nl - k0);
-            uint32_t u = (k0 + lo * a.piece_cap - pr[lo]) * 4u;
-            // lanes whose key (k0 + 64 j) passed the next piece start walk on
-            // (keys past the item, in a segment's last waves, load whatever
-            // their slot holds: count() replaces them)
+            const uint32_t q0 = q0w + ln;
+            uint32_t pl = lo, nl = pt[lo + 1];
+            int32_t t = (int32_t)(nl - q0);
+            uint32_t u = lo * a.piece_words * 4u + (q0 - pt[lo]) * 8u;
 #pragma unroll
-            for (int j = 0; j < kPartKeysPerThread; j++) {
-                if (__ballot(t <= 64 * j)) {
-                    const uint32_t k = k0 + 64u * (uint32_t)j;
-                    while (k >= nl && pl + 1 < a.fgrid) {
+            for (int j = 0; j < kJT; j++) {
+                if (__ballot(t <= 64 * j + 1)) {  // a lane at its piece's last triple or past it
+                    const uint32_t q = q0 + 64u * (uint32_t)j;
+                    while (q >= nl && pl + 1 < a.fgrid) {
                         pl++;
                         const uint32_t cl = nl;
-                        nl = pr[pl + 1];
-                        t = (int32_t)(nl - k0);
-                        u = (k0 + pl * a.piece_cap - cl) * 4u;
+                        nl = pt[pl + 1];
+                        t = (int32_t)(nl - q0);
+                        u = pl * a.piece_words * 4u + (q0 - cl) * 8u;
+                    }
+                    if (q + 1u == nl) {  // the piece's last triple: its valid keys
+                        const uint32_t vc = pk[pl + 1] - pk[pl] - 3u * (q - pt[pl]);
+                        pad |= ((vc < 3u ? 1u : 0u) | (vc < 2u ? 2u : 0u)) << (2 * j);
                     }
                 }
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, u, 256 * j, kLdAux);
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(src, u, 512 * j, kLdAux);
+                key[2 * j] = v.x;
+                key[2 * j + 1] = v.y;
             }
         } else {
             const __amdgpu_buffer_rsrc_t src =
-                uniform_rsrc(a.part1 + (uint64_t)g.base8 * kBucketAlign, (uint64_t)g.nk * 4u);
+                uniform_rsrc(a.part1 + (uint64_t)g.base8 * kBucketAlign, (uint64_t)g.nu * 4u);
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (w0 + lane) * 4u, j * 256, kLdAux);
+                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wave * kWaveKeys + lane) * 4u, j * 256, kLdAux);
         }
     };
-    // count: every key's slice counter (LDS address (key >> 12) & 0x3fc: the
-    // slice and bit 21) gets 2; the returned count is the key's byte offset in
-    // its slice run.  The ranks go to LDS (two u16 per word, [pair][thread]:
-    // conflict-free), the key becomes (counter address << 16) | its low 16
-    // bits, all that scatter() needs of it (in registers with the ranks, the
-    // scan's registers would spill, and a spill reload waits for every key
-    // load in flight).  Slots past the item (the last waves of a segment)
-    // become the dummy key of the item's bucket: bit 21 flipped, slice 0.
+    // count: every key (bucket-local, 21 bits) gets its slice counter (LDS
+    // address (key >> 12) & 0x3fc) raised by 2; the returned count is the
+    // key's byte offset in its slice run.  The ranks go to LDS (two u16 per
+    // word, [pair][thread]: conflict-free), the key becomes (counter address
+    // << 16) | its low 16 bits, all that scatter() needs of it (in registers
+    // with the ranks, the scan's registers would spill, and a spill reload
+    // waits for every key load in flight).  Slots past the item and pads
+    // become the dummy key (bit 21: counter 128).
     auto count = [&](const Item& g) {
-        const uint32_t nk = g.nk;
-        if (wave * kWaveSlots + kWaveSlots > nk) {
-            const uint32_t dummy = ((g.b & 1u) ^ 1u) << kL1Shift;
+        if (g.gath) {
+#pragma unroll
+            for (int j = kJT - 1; j >= 0; j--) {
+                const uint32_t x = key[2 * j], y = key[2 * j + 1];
+                key[3 * j] = x & kTripleMask;
+                key[3 * j + 1] = __builtin_amdgcn_alignbit(y, x, kL1Shift) & kTripleMask;
+                key[3 * j + 2] = y >> (2 * kL1Shift - 32);
+            }
+            if (__ballot(pad != 0)) {
+#pragma unroll
+                for (int j = 0; j < kJT; j++) {
+                    key[3 * j + 2] = (pad >> (2 * j)) & 1u ? kDummy : key[3 * j + 2];
+                    key[3 * j + 1] = (pad >> (2 * j)) & 2u ? kDummy : key[3 * j + 1];
+                }
+            }
+            if (wave * kWaveTriples + kWaveTriples > g.nu) {
+#pragma unroll
+                for (int j = 0; j < kJT; j++) {
+                    const bool v = wave * kWaveTriples + 64u * (uint32_t)j + lane < g.nu;
+#pragma unroll
+                    for (int i = 0; i < 3; i++)
+                        key[3 * j + i] = v ? key[3 * j + i] : kDummy;
+                }
+            }
+        } else {
+            const bool tail = wave * kWaveKeys + kWaveKeys > g.nu;
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = wave * kWaveSlots + 64u * (uint32_t)j + lane < nk ? key[j] : dummy;
+                key[j] = !tail || wave * kWaveKeys + 64u * (uint32_t)j + lane < g.nu ? key[j] & kTripleMask : kDummy;
         }
 #pragma unroll
         for (int h = 0; h < kPartKeysPerThread; h += 8) {
-            uint32_t r[8];
+            constexpr int kH = 8;
+            uint32_t r[kH];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t sa = (key[h + j] >> (kSliceBits - 2)) & ((2 * kSubs - 1) << 2);
-                r[j] = atomicAdd(&lcnt[sa >> 2], 2u);
-                key[h + j] = __builtin_amdgcn_perm(sa, key[h + j], 0x05040100u);  // sa.lo16 : key.lo16
+            for (int j = 0; j < kH; j++) {
+                if (h + j < kPartKeysPerThread) {
+                    const uint32_t sa = (key[h + j] >> (kSliceBits - 2)) & ((2 * kSubs - 1) << 2);
+                    r[j] = atomicAdd(&lcnt[sa >> 2], 2u);
+                    key[h + j] = __builtin_amdgcn_perm(sa, key[h + j], 0x05040100u);  // sa.lo16 : key.lo16
+                } else {
+                    r[j] = 0;
+                }
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < kH / 2; j++)
                 rnk[(h / 2 + j) * kPartThreads + tid] = r[2 * j] | (r[2 * j + 1] << 16);
         }
     };
     // scatter: each key's u16 to its slice run in the stage, at the run start
-    // (after the scan, loff) + its rank (the dummy slots land in [nk,
-    // kPartChunk)).  Every LDS read of a round is issued before its first use.
+    // (after the scan, loff) + its rank (the dummy slots land past the valid
+    // keys).  Every LDS read of a round is issued before its first use.
     auto scatter = [&]() {
         uint8_t* const st8 = (uint8_t*)stage;
 #pragma unroll
@@ -1748,10 +1813,13 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 rk[j] = rnk[(h / 2 + j) * kPartThreads + tid];
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                o[j] = *(const uint32_t*)((const uint8_t*)loff + (key[h + j] >> 16));
+                if (h + j < kPartKeysPerThread)
+                    o[j] = *(const uint32_t*)((const uint8_t*)loff + (key[h + j] >> 16));
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                *(uint16_t*)(st8 + o[j] + ((j & 1) ? rk[j / 2] >> 16 : rk[j / 2] & 0xffffu)) = (uint16_t)key[h + j];
+                if (h + j < kPartKeysPerThread)
+                    *(uint16_t*)(st8 + o[j] + ((j & 1) ? rk[j / 2] >> 16 : rk[j / 2] & 0xffffu)) =
+                        (uint16_t)key[h + j];
         }
     };
 
@@ -1764,20 +1832,18 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         load(g, 0);
     }
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
-        const uint32_t nk = g.nk;
         count(g);
         lds_barrier();
-        // wave 0: run starts (byte offsets in the stage) in counter order from
-        // the item's half (its slices first, then the dummy half), the item's
-        // run offsets; the counts are zeroed for the next item
+        // wave 0: run starts (byte offsets in the stage), the slices first,
+        // then the dummy counter; the item's run offsets and valid keys; the
+        // counts are zeroed for the next item
         if (wave == 0) {
-            const uint32_t q = (lane + (g.b & 1u) * (kSubs / 4)) & 63u;  // counters 4q .. 4q + 3
-            const u32x4_t c = ((const u32x4_t*)lcnt)[q];
-            ((u32x4_t*)lcnt)[q] = u32x4_t{0u, 0u, 0u, 0u};
+            const u32x4_t c = ((const u32x4_t*)lcnt)[lane];  // counters 4 lane .. 4 lane + 3
+            ((u32x4_t*)lcnt)[lane] = u32x4_t{0u, 0u, 0u, 0u};
             const uint32_t sum = c.x + c.y + c.z + c.w;
             const uint32_t ex = wave_incl_scan_dpp(sum) - sum;
             const u32x4_t o4 = {ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
-            ((u32x4_t*)loff)[q] = o4;
+            ((u32x4_t*)loff)[lane] = o4;
             uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
             if (lane < kSubs / 4) {
                 ro[4 * lane] = (uint16_t)(o4.x / 2);
@@ -1786,6 +1852,7 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
                 ro[4 * lane + 3] = (uint16_t)(o4.w / 2);
             } else if (lane == kSubs / 4) {
                 ro[kSubs] = (uint16_t)(ex / 2);
+                s_nv = ex / 2;
             }
         }
         lds_barrier();
@@ -1797,16 +1864,17 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             stage_pieces(g, pb ^ 1);
         }
         lds_barrier();
+        const uint32_t nv = s_nv;
         if (more)
             load(g, pb ^ 1);
-        // item i's keys go to part2 [i * kPartChunk, + nk) in 16-B stores
+        // item i's valid keys go to part2 [i * kPartChunk, + nv) in 16-B stores
         // (the dummy keys of the last group are never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;
         u32x4_t* dst4 = (u32x4_t*)(a.part2 + (uint64_t)item * kPartChunk);
-        for (uint32_t p = tid; p * 8u < nk; p += kPartThreads)
+        for (uint32_t p = tid; p * 8u < nv; p += kPartThreads)
             dst4[p] = st4[p];
-        // (no barrier here: the stage is rewritten only after the next item's
-        // first two barriers)
+        // (no barrier here: the stage and s_nv are rewritten only after the
+        // next item's first barrier)
     }
 }
 
