@@ -148,13 +148,14 @@ void* dqdk_gpu_queue_own_stream(dqdk_gpu_queue_t* q); /* the queue's own one */
 /* Device memory for a UMEM image or frame staging slots in HBM (the
  * device-resident and PCIe-inclusive forms).  Physically contiguous when the
  * driver allows (hipDeviceMallocContiguous; else plain device memory): the
- * decode walks frames at their UMEM stride, and from a contiguous image its
- * address translation stays within large fragments (9000 B frames: 2.27 vs
- * 2.45 ms per 1M-frame batch).  Returns 0 (contiguous), 1 (the
- * driver had no contiguous range: plain device memory) or a negative errno.
- * Allocate large images early: contiguous ranges fragment.  (The queue's own
- * table and staging are plain device memory; DQDK_GPU_CONTIG=1 makes them
- * contiguous.) */
+ * decode walks frames at their UMEM stride, and from a contiguous image it
+ * ran 9000 B batches at 2.27 instead of 2.45 ms per 1M frames on boxes in the
+ * fast state (on others every placement decodes alike).
+ * Returns 0 (contiguous), 1 (the driver had no contiguous range: plain
+ * device memory) or a negative errno.  Allocate large images early:
+ * contiguous ranges fragment.  (The queue's own table and staging are plain
+ * device memory unless DQDK_GPU_ALLOC = contig | auto: contiguous staging,
+ * auto from 128 events per frame.) */
 int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out);
 int dqdk_gpu_device_free(int device, void* d_ptr);
 
