@@ -319,11 +319,11 @@ int hist_flush(dqdk_gpu_queue* q)
 }
 
 // Windows per wave per fused round: the block's 16 waves stage at most
-// 16 * W * min(E, 128) keys per round into 284 * kFCap slots.  Measured
-// (A/B, one box): ~75 % mean fill at 1500 B (W = 16: a 64-frame tile is
-// 4 rounds; 24 with 110 % fill overflowed more than the round saved) and
-// ~115 % at 9000 B (W = 16, 2.85 vs 2.95 ms at W = 12): with every window
-// full of events, fewer rounds win over the keys that overflow to rx_part1.
+// 16 * W * min(E, 128) keys per round into 284 * kFCap slots (kFCap 120).
+// Measured (A/B, one box each): W = 16 at 1500 B (~68 % mean fill; 12 and 20
+// windows lost 1 % and 5 %), W = 12 at 9000 B, where the lines policy
+// carries up to 47 keys per bucket between rounds (16 windows overflowed
+// three times as many keys to rx_part1; 8 cost the decode more).
 //
 // The pieces' runs end mid-line.  Below 128 events per frame (1500 B) the
 // frame loads are non-temporal and the partial lines complete in L2; from
@@ -340,7 +340,7 @@ uint32_t fused_round_windows(uint32_t E)
 {
     const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
 #ifndef DQDK_FUSED_FILL
-#define DQDK_FUSED_FILL (E >= 128 ? 90 : 80)
+#define DQDK_FUSED_FILL (E >= 128 ? 80 : 75)
 #endif
     const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth

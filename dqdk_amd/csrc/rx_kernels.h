@@ -69,6 +69,12 @@ constexpr int kP1Keys = DQDK_P1_KEYS;                       // keys per thread
 constexpr int kP1Chunk = kP1Threads * kP1Keys;              // keys staged in LDS per block
 constexpr int kP1BlocksPerCu = kP1Chunk * 4 > 80 * 1024 ? 1 : 2;  // a 128-KB stage leaves room for one block
 constexpr int kP1MinWaves = kP1Threads / 64 * kP1BlocksPerCu / 4;  // waves per SIMD
+// the fused decode's overflow list: up to this many keys are added to the
+// table by atomics in rx_part1, more are grouped into rx_part2 segments
+#ifndef DQDK_OVF_ATOMIC_MAX
+#define DQDK_OVF_ATOMIC_MAX 16384
+#endif
+constexpr uint32_t kOvfAtomicMax = DQDK_OVF_ATOMIC_MAX;
 constexpr uint32_t kBucketAlign = 8;  // bucket starts in part1/part2 rounded to 8 keys (16-B part2 stores)
 constexpr uint32_t kStagePad = kL1Buckets * kBucketAlign;  // extra part1/part2 entries for that padding
 
@@ -116,7 +122,7 @@ constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one chu
 constexpr int kFWaves = 16;
 constexpr int kFThreads = kFWaves * 64;
 #ifndef DQDK_FCAP
-#define DQDK_FCAP 112
+#define DQDK_FCAP 120
 #endif
 constexpr int kFCap = DQDK_FCAP;
 constexpr uint32_t kTripleMask = (1u << kL1Shift) - 1;  // a bucket-local key

@@ -1496,8 +1496,17 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArg
     // records path: the frame-order records of the accounted frames; fused
     // path: the decode's overflow list (usually empty)
     const uint32_t total = a.total_keys ? *a.total_keys : frames_limit(a) * a.E;
+    if (a.fused && total <= kOvfAtomicMax) {
+        // a short overflow list goes straight to the table's base plane, one
+        // relaxed atomic per key (the reference's ++ at src/tristan.c:243):
+        // grouped, each bucket holding a few of its keys would cost rx_part2
+        // an item of its own
+        for (uint32_t k = blockIdx.x * kP1Threads + tid; k < total; k += gridDim.x * kP1Threads)
+            __hip_atomic_fetch_add(&a.hist[a.keys[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (total <= blockIdx.x * (uint32_t)kP1Chunk)
-        return;  // no chunk for this block (the fused path's overflow list is usually empty)
+        return;  // no chunk for this block
     uint32_t* const out = a.part1 + a.part1_base;
     const uint32_t step = gridDim.x * (uint32_t)kP1Chunk;
     uint32_t* cur1 = a.scratch + kOffCur1;
