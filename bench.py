@@ -247,7 +247,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         if name != "rx_decode":
             stages[name] = dict(s, batches=bd_steps)
     stages["rx_decode"]["batches"] = args.steps
-    hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass
+    hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass, at most
+    slice_passes = stages.get("rx_slice_histo", {}).get("launches", 0)
 
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     total_pkts = n * args.steps * world
@@ -287,9 +288,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         "rx_part2": (4 * K if pass_records else K * 8 // 3) + 2 * K + runs,
         # u16 keys + runs read, one read-modify-write of every touched slice's 16 KB of the
         # table's low-byte plane (carries into the u32 base plane: one per 256 increments)
-        # (per batch: one slice pass sweeps for hist_k staged batches)
-        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14) // max(hist_k, 1),
-        "rx_slice_heavy": 0,  # slices redone with u32 bins (none at uniform spectra); bytes counted above
+        # (per batch: one slice pass sweeps for up to hist_k staged batches; the timed
+        # batches took `slice_passes` passes, the flush inside the timed region included)
+        "rx_slice_histo": 2 * K + runs + touched * 2 * (1 << 14) * slice_passes // max(bd_steps, 1),
     }
     st = {}
     for name, s in stages.items():
@@ -322,8 +323,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                                                      0, stream.cuda_stream, 5, C.byref(ms)), "membench_frames")
         pattern["per_frame"] = round(n * (fbytes + 4 * E) / (ms.value * 1e-3) / 1e9, 1)
 
-    hist_kernels = [k for k in ("rx_histo_atomic", "rx_fixup", "rx_part1", "rx_part2", "rx_slice_histo",
-                                "rx_slice_heavy") if k in st]
+    hist_kernels = [k for k in ("rx_histo_atomic", "rx_fixup", "rx_part1", "rx_part2", "rx_slice_histo") if k in st]
     histogram = None
     if hist_kernels:
         h_ms = sum(st[k]["ms_per_batch"] for k in hist_kernels)
@@ -331,6 +331,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         gupd = K / (h_ms * 1e-3) / 1e9
         histogram = {"kernels": hist_kernels, "updates_per_batch": K, "touched_slices": touched,
                      "batches_per_slice_pass": hist_k if "rx_slice_histo" in st else None,
+                     "slice_passes": slice_passes,  # over the per-kernel breakdown's batches
                      "ms": round(h_ms, 4), "Gupd_s": round(gupd, 2),
                      # the partitioned chain streams its staging (bytes above) once per batch: its roofline
                      "streamed_bytes": h_bytes, "streamed_GB_s": round(h_bytes / (h_ms * 1e-3) / 1e9, 1),

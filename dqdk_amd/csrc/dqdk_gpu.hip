@@ -74,10 +74,10 @@ constexpr int kStages = DQDK_GPU_TIMING_STAGES;
 // (rx_fixup: on the fused path, the launch of rx_part1_kernel that takes the
 // decode's piece scans, checksum-failed frames and overflow list; stage 5 is
 // unused since rx_part2 derives its items itself)
-enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStHeavy, kStFixup };
+enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStUnused8, kStFixup };  // 5, 8: retired kernels
 const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",       "rx_histo_atomic",
                                           "rx_part1",  "(unused)", "rx_part2",       "rx_slice_histo",
-                                          "rx_slice_heavy", "rx_fixup"};
+                                          "(unused)", "rx_fixup"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
@@ -270,17 +270,13 @@ struct StageTimer {
 constexpr uint64_t kPartitionMinKeys = 4u << 20;
 
 #ifndef DQDK_HIST_KMAX
-#define DQDK_HIST_KMAX 12
-#endif
-#ifndef DQDK_HIST_SLICE_EVENTS
-#define DQDK_HIST_SLICE_EVENTS 49152
+#define DQDK_HIST_KMAX 16
 #endif
 #ifndef DQDK_HIST_STAGE_MB
-#define DQDK_HIST_STAGE_MB 16384
+#define DQDK_HIST_STAGE_MB 24576
 #endif
 constexpr size_t kHistKMax = DQDK_HIST_KMAX;  // staged batches per slice pass, at most
 static_assert(kHistKMax <= (size_t)kSliceMaxSlots, "the slice pass indexes staged batches in registers");
-constexpr size_t kHistSliceEvents = DQDK_HIST_SLICE_EVENTS;  // staged events per slice, target
 constexpr size_t kHistStageBytes = (size_t)DQDK_HIST_STAGE_MB << 20;  // staging budget of a queue
 
 bool use_partitioned(const dqdk_gpu_queue* q, uint32_t n)
@@ -309,10 +305,6 @@ int hist_flush(dqdk_gpu_queue* q)
     {
         StageTimer t(q, kStSlice);
         hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
-    }
-    {
-        StageTimer t(q, kStHeavy);  // usually an empty list: exits at once
-        hipLaunchKernelGGL(rx_slice_heavy_kernel, dim3(q->cu_count), dim3(kSliceThreads), 0, q->stream, ha);
     }
     HIPCHK(hipGetLastError());
     return 0;
@@ -735,19 +727,16 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             // part2: item i of a staged batch at [i * kPartChunk, + keys)
             q->part2_stride = (size_t)max_items(nk) * kPartChunk;
             q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
-            // Stage up to kHistKMax batches per slice pass, as many as keep a
-            // slice of uniformly spread events at about 3/4 of the 65535
-            // events of the packed-u16 form (kHistSliceEvents; the low-byte
-            // sweep is amortised over them, a fuller slice still takes the u32
-            // form) and fit the staging budget; DQDK_GPU_F_HISTO_EAGER: a
-            // pass per batch.
-            const size_t per_slice = (nk + kSlices - 1) / kSlices;
+            // Stage up to kHistKMax batches per slice pass (the low-byte sweep
+            // of a touched slice is amortised over them; the pass drains its
+            // packed-u16 bins between groups of events, so any count of
+            // events per slice fits), as many as the staging budget holds;
+            // DQDK_GPU_F_HISTO_EAGER: a pass per batch.
             const size_t slot_bytes = q->part2_stride * 2 + q->runs_stride * 2 + q->scratch_words * 4;
             q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
                             ? 1u
                             : (uint32_t)std::max<size_t>(
-                                  1, std::min({kHistKMax, kHistSliceEvents / std::max<size_t>(per_slice, 1),
-                                               kHistStageBytes / slot_bytes}));
+                                  1, std::min(kHistKMax, kHistStageBytes / slot_bytes));
             // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
             const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->dec_cus);
             const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);

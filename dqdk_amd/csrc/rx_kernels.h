@@ -22,8 +22,8 @@
  *      offsets), rx_slice_histo (gathers the slice's runs over the staged
  *      batches, packed-u16 LDS histogram, one coalesced read-modify-write of
  *      the slice's 16 KB low-byte plane, carries of 256 into the u32 base
- *      plane; slices with more than 65535 events are listed and redone with
- *      u32 LDS bins by rx_slice_heavy).  The table is held as value =
+ *      plane; bins are drained into the base plane between groups of 65280
+ *      events, so any spectrum fits the u16 bins).  The table is held as value =
  *      base[bin] + low[bin] (mod 2^32): the same values as the reference's
  *      u32 table, with a 4x smaller per-pass sweep.
  */
@@ -49,7 +49,7 @@ constexpr int kFRingW = DQDK_FRINGW;  // the same for the fused decode (rounds a
 // Partitioned histogram geometry.  Keys < 1512*6*65536 = 594,542,592 < 2^30.
 constexpr int kL1Shift = 21;                                // 2^21 bins (8 MB of table) per bucket
 constexpr int kL1Buckets = 284;                             // ceil(594542592 / 2^21)
-constexpr int kSliceBits = 14;                              // 2^14 bins per slice (32 KB packed-u16 LDS; 64 KB in the u32 form)
+constexpr int kSliceBits = 14;                              // 2^14 bins per slice (32 KB packed-u16 LDS)
 constexpr int kSubs = 1 << (kL1Shift - kSliceBits);         // 128 slices per bucket
 constexpr int kSlices = kL1Buckets * kSubs;                 // 36352 (36288 used)
 constexpr int kPartThreads = 1024;                          // part1/part2 block size
@@ -82,7 +82,6 @@ constexpr uint32_t kStagePad = kL1Buckets * kBucketAlign;  // extra part1/part2 
 constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket: decode upper bound (records path) or
                                     //   overflow keys per bucket (fused path)                 -- zeroed per batch
 constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket by rx_part1         -- zeroed per batch
-constexpr int kOffHeavyN = 576;     // slices listed for the u32 slice form                     -- zeroed per batch
 constexpr int kOffOvfN = 577;       // fused path: keys sent to the overflow list               -- zeroed per batch
 constexpr int kOffFixN = 578;       // fused path: decoded frames whose final status is not OK  -- zeroed per batch
 constexpr int kZeroWords = 584;
@@ -103,9 +102,8 @@ __host__ __device__ constexpr uint64_t max_items(uint64_t nk)
 {
     return nk / kPartChunk + (uint64_t)kL1Buckets * (kSegsPerBucket + 1) + 1;
 }
-constexpr int kOffHeavyList = kOffEnd;  // [kSlices] (slot 0 of a slice pass) slices redone in u32
 // u32 words of one staged slot's scratch
-constexpr uint64_t kHistScratchWords = kOffHeavyList + kSlices;
+constexpr uint64_t kHistScratchWords = kOffEnd;
 constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one chunk of a segment)
 
 // Fused decode (rx_decode_fused): 1024-thread blocks, one per CU, persistent.
@@ -223,6 +221,5 @@ __global__ void rx_part1_kernel(RxArgs ra, HistoArgs a);
 template <int kLdAux>
 __global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);
-__global__ void rx_slice_heavy_kernel(HistoArgs a);
 
 }  // namespace dqdk

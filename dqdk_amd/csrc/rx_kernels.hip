@@ -1897,27 +1897,28 @@ template __global__ void rx_part2_kernel<2>(HistoArgs);
 // written once after the LDS histogram is complete, with carries of 256
 // into the u32 base plane (rare: one per 256 increments of a bin).
 //
-// Two forms share the code: the common one counts in packed u16 LDS bins
-// (32 KB: four blocks per CU hide the gather latency), valid while the
-// slice receives at most 65535 events in the batch; a slice with more
-// (skewed spectra, hot bins) is appended to a list and redone by the u32
-// form (64 KB LDS) in a second launch over that list.
+// The bins are packed u16 pairs (32 KB: four blocks per CU hide the gather
+// latency).  A bin cannot pass 65535: the runs are counted in groups of at
+// most 65280 events, and between two groups every bin's high byte is
+// drained into the base plane (an LDS sweep; a global add only where a bin
+// reached 256), so any number of staged batches and any spectrum -- hot
+// bins included -- is counted in one pass.
 struct SliceLds {
-    uint32_t s_lo[kSliceThreads], s_hi[kSliceThreads], s_base[kSliceThreads];  // run [lo, hi) of item s_base
+    uint32_t s_run[kSliceThreads];  // lo | hi << 16: the run [lo, hi) of item s_base (u16 offsets)
+    uint32_t s_pin[kSliceThreads];  // inclusive prefix of the run lengths of the staged entries
+    uint32_t s_base[kSliceThreads];
     uint8_t s_k[kSliceThreads];
     uint32_t b_i0[kSliceMaxSlots], b_n[kSliceMaxSlots];  // the bucket's first item / items per staged batch
+    uint32_t w_tot[kSliceThreads / 64];
     uint32_t total;
 };
+constexpr uint32_t kDrainCap = 0xffffu - 0xffu;  // events per group: bins hold <= 255 after a drain
 
 constexpr uint32_t kSliceMask = (1u << kSliceBits) - 1;
 
-template <bool kPacked>
 __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
 {
-    if (kPacked)
-        atomicAdd(&h[k >> 1], 1u << ((k & 1u) << 4));
-    else
-        atomicAdd(&h[k], 1u);
+    atomicAdd(&h[k >> 1], 1u << ((k & 1u) << 4));
 }
 
 // The runs of one slice over every staged batch form one flat list of
@@ -1925,11 +1926,10 @@ __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
 // ...; entries [e0, e0 + n) are staged in LDS by one round of loads
 // (kSliceMaxSlots: rx_kernels.h)
 
-// counters: packed ? u16 pairs (8192 words) : u32 (16384 words)
-template <bool kPacked>
+// counters: u16 pairs (8192 words)
 __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint32_t* h, SliceLds& sl)
 {
-    constexpr int kWords = kPacked ? (1 << kSliceBits) / 2 : (1 << kSliceBits);
+    constexpr int kWords = (1 << kSliceBits) / 2;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     constexpr int kWavesS = kSliceThreads / 64;
@@ -1981,8 +1981,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             locate(e0 + (uint32_t)tid, k, it);
             const uint16_t* ro = runs(k) + (uint64_t)it * kItemOffs + sub;
             const uint32_t lo = ro[0], hi = ro[1];
-            sl.s_lo[tid] = lo;
-            sl.s_hi[tid] = hi;
+            sl.s_run[tid] = lo | (hi << 16);
             sl.s_base[tid] = it;
             sl.s_k[tid] = (uint8_t)k;
             mine = hi - lo;
@@ -1998,18 +1997,14 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     uint32_t mine = 0;
     for (uint32_t e0 = (uint32_t)kSliceThreads; e0 < nent; e0 += kSliceThreads)
         mine += stage(e0, min(nent - e0, (uint32_t)kSliceThreads));
-    mine += stage(0, min(nent, (uint32_t)kSliceThreads));
+    const uint32_t mine0 = stage(0, min(nent, (uint32_t)kSliceThreads));
+    mine += mine0;
     if (mine)
         atomicAdd(&sl.total, mine);
     __syncthreads();
     const uint32_t total = sl.total;
     if (total == 0)
         return;  // no events for this slice: table untouched
-    if (kPacked && total > 0xffffu) {  // a u16 bin could overflow: the u32 form redoes it
-        if (tid == 0)
-            a.scratch[kOffHeavyList + atomicAdd(&a.scratch[kOffHeavyN], 1u)] = s;
-        return;
-    }
     const uint64_t sb = (uint64_t)s << kSliceBits;
     u32x4_t* lo4 = (u32x4_t*)(a.lo + sb);
     constexpr int kLoPer = (1 << kSliceBits) / 16 / kSliceThreads;  // 2 x 16 B per thread
@@ -2029,24 +2024,69 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
 #endif
     constexpr int kNI = DQDK_SLICE_NI;
     constexpr int kKG = DQDK_SLICE_KG;
+    // packed bins: move every bin's high byte into the base plane (bins left
+    // <= 255).  Thread t owns bins [16t, 16t + 16) and [16(t + 512), +16) here
+    // and in the final read-modify-write, so its plain global adds are ordered.
+    auto drain = [&]() {
+#pragma unroll
+        for (int j = 0; j < kLoPer; j++) {
+            const uint32_t b0 = 16u * (uint32_t)(tid + j * kSliceThreads);
+            u32x4_t* hc = (u32x4_t*)(h + b0 / 2);
+            const u32x4_t c0 = hc[0], c1 = hc[1];
+            uint32_t w8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            uint32_t any = 0;
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                uint32_t& w = w8[m];
+                const uint32_t hw = w & 0xff00ff00u;
+                if (hw) {
+                    if (hw & 0xffffu)
+                        a.hist[sb + b0 + 2 * m] += hw & 0xffffu;
+                    if (hw >> 16)
+                        a.hist[sb + b0 + 2 * m + 1] += hw >> 16;
+                    w &= 0x00ff00ffu;
+                }
+                any |= hw;
+            }
+            if (any) {
+                hc[0] = u32x4_t{w8[0], w8[1], w8[2], w8[3]};
+                hc[1] = u32x4_t{w8[4], w8[5], w8[6], w8[7]};
+            }
+        }
+    };
+    const bool drains = total > kDrainCap;  // else one group: no bin can pass 65535
+    uint32_t since = 0;  // events counted since the last drain (block-uniform)
     for (uint32_t e0 = 0; e0 < nent; e0 += kSliceThreads) {
         const uint32_t nit = min(nent - e0, (uint32_t)kSliceThreads);
-        if (e0 != 0) {  // more than 512 entries (skewed data, many staged batches)
+        uint32_t m = mine0;
+        if (e0 != 0) {  // more than 512 entries (many staged batches, skewed data)
             __syncthreads();
-            stage(e0, nit);
-            __syncthreads();
+            m = stage(e0, nit);
         }
+        if (drains) {  // inclusive prefix of the run lengths over the chunk's entries
+            const uint32_t inc = wave_incl_scan_dpp(m);
+            if (lane == 63)
+                sl.w_tot[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int q = 0; q < kWavesS; q++)
+                off += q < wave ? sl.w_tot[q] : 0u;
+            sl.s_pin[tid] = off + inc;
+        }
+        __syncthreads();
         // a group = the kNI items j, j + kWavesS, ... of one wave.  Item run
         // parameters are wave-uniform and re-read from LDS where needed, so
         // nothing but the loaded dwords is live across a group's loads
         // (64 VGPRs: 4 blocks per CU).  Issuing the next group's loads before
         // counting this one's measured slower.
         constexpr uint32_t kGrp = kNI * kWavesS;
+        uint32_t ge = nit;  // entries [gs, ge): the current group
         auto run = [&](uint32_t jj, uint32_t& klo, uint32_t& khi) {
-            const bool v = jj < nit;
-            const uint32_t jc = v ? jj : 0u;
-            klo = v ? rfl(sl.s_lo[jc]) : 0u;
-            khi = v ? rfl(sl.s_hi[jc]) : 0u;
+            const bool v = jj < ge;
+            const uint32_t r = rfl(sl.s_run[v ? jj : 0u]);
+            klo = v ? r & 0xffffu : 0u;
+            khi = v ? r >> 16 : 0u;
         };
         // a buffer descriptor per item whose extent ends at the run's last
         // dword (so the loads need no per-lane bound); items start at
@@ -2058,7 +2098,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 const uint32_t jj = j + q * kWavesS;
                 uint32_t klo, khi;
                 run(jj, klo, khi);
-                const uint32_t jc = jj < nit ? jj : 0u;
+                const uint32_t jc = jj < ge ? jj : 0u;
                 const uint32_t dlo = klo >> 1, dhi = (khi + 1) >> 1;
                 const uint16_t* base = a.part2 + (uint64_t)rfl(sl.s_k[jc]) * a.part2_stride +
                                        (uint64_t)rfl(sl.s_base[jc]) * kPartChunk;
@@ -2081,20 +2121,42 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                     const uint32_t k0 = 2 * (dlo + p0 + 64 * g + lane);  // key index of the low half
                     // (part2 stores a key's low 16 bits: bits 14-15 are its slice's)
                     if (k0 >= klo && k0 < khi)
-                        slice_count<kPacked>(h, w[q][g] & kSliceMask);
+                        slice_count(h, w[q][g] & kSliceMask);
                     if (k0 + 1 >= klo && k0 + 1 < khi)
-                        slice_count<kPacked>(h, (w[q][g] >> 16) & kSliceMask);
+                        slice_count(h, (w[q][g] >> 16) & kSliceMask);
                 }
             }
         };
-        for (uint32_t j = (uint32_t)wave; j < nit; j += kGrp) {
-            uint32_t w[kNI][kKG];
-            const uint32_t steps = issue(j, 0, w);
-            count(j, 0, w);
-            for (uint32_t p0 = 64 * kKG; p0 < steps; p0 += 64 * kKG) {  // runs longer than one pass (rare)
-                issue(j, p0, w);
-                count(j, p0, w);
+        for (uint32_t gs = 0; gs < nit;) {
+            if (drains) {  // the group: the longest run of entries whose events fit kDrainCap - since
+                const uint32_t base = gs ? rfl(sl.s_pin[gs - 1]) : 0u, lim = kDrainCap - since;
+                uint32_t lo = gs, hi = nit;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (rfl(sl.s_pin[mid]) - base > lim)
+                        hi = mid;
+                    else
+                        lo = mid + 1;
+                }
+                ge = (lo == gs && since == 0) ? gs + 1 : lo;  // (a run never passes the cap alone)
+                since += ge > gs ? rfl(sl.s_pin[ge - 1]) - base : 0u;
             }
+            for (uint32_t j = gs + (uint32_t)wave; j < ge; j += kGrp) {
+                uint32_t w[kNI][kKG];
+                const uint32_t steps = issue(j, 0, w);
+                count(j, 0, w);
+                for (uint32_t p0 = 64 * kKG; p0 < steps; p0 += 64 * kKG) {  // runs longer than one pass (rare)
+                    issue(j, p0, w);
+                    count(j, p0, w);
+                }
+            }
+            if (ge < nit) {  // the next run would pass the cap
+                __syncthreads();
+                drain();
+                __syncthreads();
+                since = 0;
+            }
+            gs = ge;
         }
     }
     __syncthreads();
@@ -2103,7 +2165,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     for (int j = 0; j < kLoPer; j++) {
         const uint32_t b0 = 16u * (uint32_t)(tid + j * kSliceThreads);
         uint32_t incs[16];
-        if (kPacked) {
+        {
             const u32x4_t* hc = (const u32x4_t*)(h + b0 / 2);
             const u32x4_t c0 = hc[0], c1 = hc[1];
             const uint32_t w8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
@@ -2111,16 +2173,6 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             for (int m = 0; m < 8; m++) {
                 incs[2 * m] = w8[m] & 0xffffu;
                 incs[2 * m + 1] = w8[m] >> 16;
-            }
-        } else {
-            const u32x4_t* hc = (const u32x4_t*)(h + b0);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const u32x4_t c = hc[k];
-                incs[4 * k] = c.x;
-                incs[4 * k + 1] = c.y;
-                incs[4 * k + 2] = c.z;
-                incs[4 * k + 3] = c.w;
             }
         }
         uint32_t words[4] = {l[j].x, l[j].y, l[j].z, l[j].w};
@@ -2145,19 +2197,7 @@ __global__ void __launch_bounds__(kSliceThreads, 8) rx_slice_histo_kernel(HistoA
 {
     __shared__ __attribute__((aligned(16))) uint32_t h[(1 << kSliceBits) / 2];
     __shared__ SliceLds sl;
-    slice_histo<true>(a, blockIdx.x, h, sl);
-}
-
-// Slices with more than 65535 events in the batch (listed by the packed form).
-__global__ void __launch_bounds__(kSliceThreads) rx_slice_heavy_kernel(HistoArgs a)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t h[1 << kSliceBits];
-    __shared__ SliceLds sl;
-    const uint32_t n = a.scratch[kOffHeavyN];
-    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-        slice_histo<false>(a, a.scratch[kOffHeavyList + k], h, sl);
-        __syncthreads();
-    }
+    slice_histo(a, blockIdx.x, h, sl);
 }
 
 }  // namespace dqdk

@@ -296,7 +296,7 @@ int dqdk_gpu_membench_frames(const void* d_umem, uint64_t stride, uint32_t frame
  * pair of hipEvents on the queue stream; stage k is one kernel, named by
  * dqdk_gpu_timing_stage_name(k):
  *   0 rx_decode (or the fused decode)  1 rx_abort  2 rx_count  3 rx_histo_atomic
- *   4 rx_part1   5 (unused)  6 rx_part2  7 rx_slice_histo  8 rx_slice_heavy
+ *   4 rx_part1   5 (unused)  6 rx_part2  7 rx_slice_histo  8 (unused)
  *   9 rx_fixup (fused path: the rx_part1 launch that takes the decode's piece
  *     sizes, its decoded frames whose final status is not OK and its overflow list)
  * timing_read adds up the completed pairs (after syncing the queue stream),
