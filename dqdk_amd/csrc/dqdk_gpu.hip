@@ -304,7 +304,7 @@ int hist_flush(dqdk_gpu_queue* q)
     q->hist_pending = 0;
     {
         StageTimer t(q, kStSlice);
-        hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSlices), dim3(kSliceThreads), 0, q->stream, ha);
+        hipLaunchKernelGGL(rx_slice_histo_kernel, dim3(kSliceBlocks), dim3(kSliceThreads), 0, q->stream, ha);
     }
     HIPCHK(hipGetLastError());
     return 0;

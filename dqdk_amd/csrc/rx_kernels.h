@@ -56,7 +56,12 @@ constexpr int kPartThreads = 1024;                          // part1/part2 block
 constexpr int kPartKeysPerThread = 15;                      // five key triples per lane
 constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 15360 key slots staged in LDS (an item)
 constexpr int kPartTriples = kPartChunk / 3;                // 5120 triples: a gathered item
-constexpr int kSliceThreads = 512;
+#ifndef DQDK_SLICE_SPAN
+#define DQDK_SLICE_SPAN 2
+#endif
+constexpr int kSliceSpan = DQDK_SLICE_SPAN;      // adjacent slices per slice-pass block (their runs are adjacent too)
+constexpr int kSliceThreads = 512 * kSliceSpan;  // 32 waves per CU either way
+constexpr int kSliceBlocks = kSlices / kSliceSpan;
 constexpr int kSliceMaxSlots = 16;  // staged batches one slice pass can take
 #ifndef DQDK_P1_KEYS
 #define DQDK_P1_KEYS 32

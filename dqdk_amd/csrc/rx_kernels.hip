@@ -1890,15 +1890,18 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
 template __global__ void rx_part2_kernel<0>(HistoArgs);
 template __global__ void rx_part2_kernel<2>(HistoArgs);
 
-// Level 3: one block per 16K-bin slice.  The run offsets of the bucket's
-// items (<= 512 at a time) are staged in LDS first, so gathering a run is
-// one dependent load, and each wave gathers four items at once; the slice's
-// 16 KB of the table's low-byte plane is loaded up front and read-modify-
-// written once after the LDS histogram is complete, with carries of 256
-// into the u32 base plane (rare: one per 256 increments of a bin).
+// Level 3: one block per span of kSliceSpan (2) adjacent 16K-bin slices:
+// within a part2 item their runs are adjacent, so one run of ~240 keys per
+// item and span (a latency-bound gather: twice the bytes per load round of a
+// one-slice block).  The run offsets of the bucket's items (<= kSliceThreads
+// at a time) are staged in LDS first, so gathering a run is one dependent
+// load, and each wave gathers three items at once; the span's 32 KB of the
+// table's low-byte plane is loaded up front and read-modify-written once
+// after the LDS histogram is complete, with carries of 256 into the u32 base
+// plane (rare: one per 256 increments of a bin).
 //
-// The bins are packed u16 pairs (32 KB: four blocks per CU hide the gather
-// latency).  A bin cannot pass 65535: the runs are counted in groups of at
+// The bins are packed u16 pairs (64 KB: two 1024-thread blocks per CU, 32
+// waves, hide the gather latency).  A bin cannot pass 65535: the runs are counted in groups of at
 // most 65280 events, and between two groups every bin's high byte is
 // drained into the base plane (an LDS sweep; a global add only where a bin
 // reached 256), so any number of staged batches and any spectrum -- hot
@@ -1914,7 +1917,7 @@ struct SliceLds {
 };
 constexpr uint32_t kDrainCap = 0xffffu - 0xffu;  // events per group: bins hold <= 255 after a drain
 
-constexpr uint32_t kSliceMask = (1u << kSliceBits) - 1;
+constexpr uint32_t kSpanMask = ((uint32_t)kSliceSpan << kSliceBits) - 1;  // a key's bin in its block's span
 
 __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
 {
@@ -1929,10 +1932,11 @@ __device__ __forceinline__ void slice_count(uint32_t* h, uint32_t k)
 // counters: u16 pairs (8192 words)
 __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint32_t* h, SliceLds& sl)
 {
-    constexpr int kWords = (1 << kSliceBits) / 2;
+    constexpr int kWords = (kSliceSpan << kSliceBits) / 2;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     constexpr int kWavesS = kSliceThreads / 64;
+    s *= kSliceSpan;  // the span's first slice
     const uint32_t b = s / kSubs, sub = s % kSubs;
     // staged batch k: its scratch (bucket starts, item starts), u16 keys, run offsets
     auto sc = [&](uint32_t k) { return a.scratch + (uint64_t)k * a.scratch_stride; };
@@ -1980,7 +1984,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             uint32_t k, it;
             locate(e0 + (uint32_t)tid, k, it);
             const uint16_t* ro = runs(k) + (uint64_t)it * kItemOffs + sub;
-            const uint32_t lo = ro[0], hi = ro[1];
+            const uint32_t lo = ro[0], hi = ro[kSliceSpan];
             sl.s_run[tid] = lo | (hi << 16);
             sl.s_base[tid] = it;
             sl.s_k[tid] = (uint8_t)k;
@@ -2007,25 +2011,25 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         return;  // no events for this slice: table untouched
     const uint64_t sb = (uint64_t)s << kSliceBits;
     u32x4_t* lo4 = (u32x4_t*)(a.lo + sb);
-    constexpr int kLoPer = (1 << kSliceBits) / 16 / kSliceThreads;  // 2 x 16 B per thread
+    constexpr int kLoPer = (kSliceSpan << kSliceBits) / 16 / kSliceThreads;  // 2 x 16 B per thread
     u32x4_t l[kLoPer];
 #pragma unroll
     for (int j = 0; j < kLoPer; j++)
         l[j] = lo4[tid + j * kSliceThreads];
     // each wave gathers kNI items at once, kKG dwords (two keys) per lane per
-    // item per pass (256 keys: a whole typical run), so a block takes its
+    // item per pass (384 keys: a whole typical span run), so a block takes its
     // items in rounds of kNI * kWavesS; runs start at any key: dword loads
     // from the run's first even key, halves outside the run are dropped
 #ifndef DQDK_SLICE_NI
-#define DQDK_SLICE_NI 4
+#define DQDK_SLICE_NI 3
 #endif
 #ifndef DQDK_SLICE_KG
-#define DQDK_SLICE_KG 2
+#define DQDK_SLICE_KG 3
 #endif
     constexpr int kNI = DQDK_SLICE_NI;
     constexpr int kKG = DQDK_SLICE_KG;
     // packed bins: move every bin's high byte into the base plane (bins left
-    // <= 255).  Thread t owns bins [16t, 16t + 16) and [16(t + 512), +16) here
+    // <= 255).  Thread t owns bins [16t, +16) and [16(t + kSliceThreads), +16) here
     // and in the final read-modify-write, so its plain global adds are ordered.
     auto drain = [&]() {
 #pragma unroll
@@ -2078,7 +2082,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         // a group = the kNI items j, j + kWavesS, ... of one wave.  Item run
         // parameters are wave-uniform and re-read from LDS where needed, so
         // nothing but the loaded dwords is live across a group's loads
-        // (64 VGPRs: 4 blocks per CU).  Issuing the next group's loads before
+        // (64 VGPRs: 32 waves per CU).  Issuing the next group's loads before
         // counting this one's measured slower.
         constexpr uint32_t kGrp = kNI * kWavesS;
         uint32_t ge = nit;  // entries [gs, ge): the current group
@@ -2121,9 +2125,9 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                     const uint32_t k0 = 2 * (dlo + p0 + 64 * g + lane);  // key index of the low half
                     // (part2 stores a key's low 16 bits: bits 14-15 are its slice's)
                     if (k0 >= klo && k0 < khi)
-                        slice_count(h, w[q][g] & kSliceMask);
+                        slice_count(h, w[q][g] & kSpanMask);
                     if (k0 + 1 >= klo && k0 + 1 < khi)
-                        slice_count(h, (w[q][g] >> 16) & kSliceMask);
+                        slice_count(h, (w[q][g] >> 16) & kSpanMask);
                 }
             }
         };
@@ -2160,7 +2164,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         }
     }
     __syncthreads();
-    // low-byte plane: thread t owns bins [16t, 16t + 16) and [16(t + 512), +16)
+    // low-byte plane: thread t owns bins [16t, +16) and [16(t + kSliceThreads), +16)
 #pragma unroll
     for (int j = 0; j < kLoPer; j++) {
         const uint32_t b0 = 16u * (uint32_t)(tid + j * kSliceThreads);
@@ -2193,9 +2197,9 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     }
 }
 
-__global__ void __launch_bounds__(kSliceThreads, 8) rx_slice_histo_kernel(HistoArgs a)  // 4 blocks per CU
+__global__ void __launch_bounds__(kSliceThreads, 8) rx_slice_histo_kernel(HistoArgs a)  // 32 waves per CU
 {
-    __shared__ __attribute__((aligned(16))) uint32_t h[(1 << kSliceBits) / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t h[(kSliceSpan << kSliceBits) / 2];
     __shared__ SliceLds sl;
     slice_histo(a, blockIdx.x, h, sl);
 }
