@@ -1848,7 +1848,9 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
         // counts are zeroed for the next item
         if (wave == 0) {
             const u32x4_t c = ((const u32x4_t*)lcnt)[lane];  // counters 4 lane .. 4 lane + 3
-            ((u32x4_t*)lcnt)[lane] = u32x4_t{0u, 0u, 0u, 0u};
+            uint32_t z = 0;
+            asm volatile("" : "+v"(z));  // (a zero vector hoisted out of the item loop spills)
+            ((u32x4_t*)lcnt)[lane] = u32x4_t{z, z, z, z};
             const uint32_t sum = c.x + c.y + c.z + c.w;
             const uint32_t ex = wave_incl_scan_dpp(sum) - sum;
             const u32x4_t o4 = {ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
