@@ -53,7 +53,7 @@ METRIC = "Mpkt/s & GB/s device-resident UDP/IP parse+TRISTAN decode, 1500B & 900
 def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # 32 = two whole slice passes of 16 staged batches (the steady state of a
+    # 32 = one whole slice pass of 32 staged batches at 1500 B (the steady state of a
     # long capture: one pass per histogram_batches_per_pass() batches)
     p.add_argument("--steps", type=int, default=32)
     p.add_argument("--warmup", type=int, default=3)
@@ -237,7 +237,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
 
     # per-kernel breakdown: an extra pass (outside the timed region) with every
     # launch bracketed; rx_decode keeps its timed-region figure
-    bd_steps = min(args.steps, 16)  # one whole slice pass
+    bd_steps = min(args.steps, 16)
     q.timing_stages(None)
     q.enable_timing(True)
     for _ in range(bd_steps):

@@ -270,7 +270,7 @@ struct StageTimer {
 constexpr uint64_t kPartitionMinKeys = 4u << 20;
 
 #ifndef DQDK_HIST_KMAX
-#define DQDK_HIST_KMAX 16
+#define DQDK_HIST_KMAX 32
 #endif
 #ifndef DQDK_HIST_STAGE_MB
 #define DQDK_HIST_STAGE_MB 24576

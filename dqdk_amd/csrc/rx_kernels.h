@@ -62,7 +62,7 @@ constexpr int kPartTriples = kPartChunk / 3;                // 5120 triples: a g
 constexpr int kSliceSpan = DQDK_SLICE_SPAN;      // adjacent slices per slice-pass block (their runs are adjacent too)
 constexpr int kSliceThreads = 512 * kSliceSpan;  // 32 waves per CU either way
 constexpr int kSliceBlocks = kSlices / kSliceSpan;
-constexpr int kSliceMaxSlots = 16;  // staged batches one slice pass can take
+constexpr int kSliceMaxSlots = 32;  // staged batches one slice pass can take
 #ifndef DQDK_P1_KEYS
 #define DQDK_P1_KEYS 32
 #endif

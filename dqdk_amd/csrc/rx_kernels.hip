@@ -1913,7 +1913,7 @@ struct SliceLds {
     uint32_t s_pin[kSliceThreads];  // inclusive prefix of the run lengths of the staged entries
     uint32_t s_base[kSliceThreads];
     uint8_t s_k[kSliceThreads];
-    uint32_t b_i0[kSliceMaxSlots], b_n[kSliceMaxSlots];  // the bucket's first item / items per staged batch
+    uint32_t b_i0[kSliceMaxSlots], b_end[kSliceMaxSlots];  // the bucket's first item / inclusive prefix of its items per staged batch
     uint32_t w_tot[kSliceThreads / 64];
     uint32_t total;
 };
@@ -1943,15 +1943,20 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     // staged batch k: its scratch (bucket starts, item starts), u16 keys, run offsets
     auto sc = [&](uint32_t k) { return a.scratch + (uint64_t)k * a.scratch_stride; };
     auto runs = [&](uint32_t k) { return a.runs + (uint64_t)k * a.runs_stride; };
-    // the bucket's items per staged batch (LDS: registers would be 32 more)
-    if (tid < kSliceMaxSlots) {
+    // the bucket's items per staged batch and their running total (LDS:
+    // registers would be 64 more)
+    static_assert(kSliceMaxSlots == 32, "one wave scans the staged batches; locate() searches 2^5 of them");
+    if (tid < 64) {
         uint32_t i0 = 0, n = 0;
         if ((uint32_t)tid < a.nslots) {
             i0 = sc(tid)[kOffIstart + b];
             n = sc(tid)[kOffIstart + b + 1] - i0;
         }
-        sl.b_i0[tid] = i0;
-        sl.b_n[tid] = n;
+        const uint32_t end = wave_incl_scan_dpp(n);
+        if (tid < kSliceMaxSlots) {
+            sl.b_i0[tid] = i0;
+            sl.b_end[tid] = end;
+        }
     }
     if (tid == 0)
         sl.total = 0;
@@ -1959,25 +1964,23 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
     for (int c = tid; c < kWords / 4; c += kSliceThreads)
         h4[c] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
-    uint32_t nent = 0;
-#pragma unroll
-    for (int k = 0; k < kSliceMaxSlots; k++)
-        nent += sl.b_n[k];
+    const uint32_t nent = sl.b_end[kSliceMaxSlots - 1];
     if (nent == 0)
         return;
-    // entry e (< nent) -> its batch k and item
+    // entry e (< nent) -> its batch k (the first whose running total passes
+    // e: a binary search) and item
     auto locate = [&](uint32_t e, uint32_t& k, uint32_t& it) {
-        uint32_t kk = 0, rest = e;
+        uint32_t lo = 0, hi = kSliceMaxSlots - 1;
 #pragma unroll
-        for (int q = 0; q < kSliceMaxSlots; q++) {
-            const uint32_t n = sl.b_n[q];
-            if (kk == (uint32_t)q && rest >= n) {
-                rest -= n;
-                kk++;
-            }
+        for (int s2 = 0; s2 < 5; s2++) {  // 2^5 = kSliceMaxSlots candidates
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sl.b_end[mid] > e)
+                hi = mid;
+            else
+                lo = mid + 1;
         }
-        k = kk;
-        it = sl.b_i0[kk] + rest;
+        k = lo;
+        it = sl.b_i0[lo] + e - (lo ? sl.b_end[lo - 1] : 0u);
     };
     // entries [e0, e0 + ne) -> LDS: run bounds, item base, batch
     auto stage = [&](uint32_t e0, uint32_t ne) -> uint32_t {
@@ -1994,7 +1997,7 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
         }
         return mine;
     };
-    // s_lo..s_k are written below only after every thread has read b_n
+    // s_run..s_k are written below only after every thread has read b_end
     __syncthreads();
     // events of this slice = sum of its run lengths: from the first staged
     // chunk of entries when it holds them all (the usual case), else a pass

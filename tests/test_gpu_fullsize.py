@@ -150,17 +150,18 @@ def test_records_path_full_size_vs_oracle():
     np.testing.assert_array_equal(keys.reshape(n, E)[ok], okeys.reshape(n, E)[ok])
 
 
-def test_slice_pass_over_sixteen_staged_batches():
-    """256K x 9000 B batches (configs[2]) staged sixteen deep: one slice pass
-    takes ~540 runs per slice (more than one 512-entry chunk of its LDS) and
-    ~250K events per slice, so its packed-u16 bins are drained into the base
-    plane between groups several times.  The same batch sixteen times: the
-    table is sixteen times the oracle's."""
-    n, k = 1 << 18, 16
+def test_slice_pass_over_a_full_stage_of_batches():
+    """256K x 9000 B batches (configs[2]) staged as deep as the queue allows
+    (32): one slice pass takes ~1100 runs per two-slice span (more than one
+    1024-entry chunk of its LDS) and ~1M events per span, so its packed-u16
+    bins are drained into the base plane between groups many times.  The
+    same batch k times: the table is k times the oracle's."""
+    n = 1 << 18
     umem, desc = D.synth_umem(n, 9000, 9216, faulty=True, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=8958, flags=D.F_CSUM)
     with D.RxQueue(0, cfg, n) as q:
-        assert q.histogram_batches_per_pass() == k
+        k = q.histogram_batches_per_pass()
+    assert k == 32
     res, cnt, table, launches = run_bench_form(umem, desc, cfg, batches=k)
     assert launches.get("rx_fixup", 0) == k and launches.get("rx_slice_histo", 0) == 1, launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
