@@ -237,7 +237,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
 
     # per-kernel breakdown: an extra pass (outside the timed region) with every
     # launch bracketed; rx_decode keeps its timed-region figure
-    bd_steps = min(args.steps, 16)
+    bd_steps = min(args.steps, 32)  # the timed region's slice-pass cadence (32 staged batches at 1500 B)
     q.timing_stages(None)
     q.enable_timing(True)
     for _ in range(bd_steps):
