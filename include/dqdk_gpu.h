@@ -236,8 +236,8 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
 /* Partitioned batches stage their slice-sorted events and the slice pass
  * (the sweep of the table's low-byte plane) runs once per
- * batches_per_pass staged batches (up to 12, while a 16K-bin slice of
- * uniformly spread events stays under 48K events; DQDK_GPU_F_HISTO_EAGER:
+ * batches_per_pass staged batches (up to 32, as many as a 24 GB staging
+ * budget holds: 32 at 1M x 1500 B, 20 at 1M x 9000 B; DQDK_GPU_F_HISTO_EAGER:
  * 1).  Every histogram reader above and below flushes first; flush runs
  * the pending slice pass now (async on the queue stream). */
 int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q);
