@@ -12,10 +12,10 @@ from ._lib import (F_HISTO_ATOMIC, F_HISTO_EAGER, F_HISTO_UNFUSED, F_HISTO_PARTI
                    RX_EMPTY, RX_FILTER_DROP, RX_FILTER_PASS, RX_INVALID_IP, RX_INVALID_IP_CSUM,
                    RX_INVALID_UDP, RX_INVALID_UDP_CSUM, RX_OK, DESC_DTYPE, RESULT_DTYPE, HISTO_ENTRIES,
                    DqdkError)
-from .rx import DeviceBuffer, RxConfig, RxQueue, device_count, events_per_payload, histo_enabled, synth_umem, tristan_summary, SEED
+from .rx import DeviceBuffer, FrameProcessor, RxConfig, RxQueue, device_count, events_per_payload, histo_enabled, synth_umem, tristan_summary, SEED
 
 __all__ = [
-    "DeviceBuffer", "RxConfig", "RxQueue", "device_count", "events_per_payload", "histo_enabled", "synth_umem", "tristan_summary", "SEED",
+    "DeviceBuffer", "FrameProcessor", "RxConfig", "RxQueue", "device_count", "events_per_payload", "histo_enabled", "synth_umem", "tristan_summary", "SEED",
     "DESC_DTYPE", "RESULT_DTYPE", "HISTO_ENTRIES", "KEY_NONE", "MODES", "DqdkError",
     "F_CSUM", "F_BATCH_ABORT", "F_HISTO_ATOMIC", "F_HISTO_UNFUSED", "F_HISTO_PARTITIONED", "F_HISTO_EAGER", "F_PREFILTER", "F_NO_HISTO", "F_CSUM_WRITEBACK",
     "MODE_WAVEFORM", "MODE_LISTWAVE", "MODE_LISTMODE", "MODE_ENERGYHISTO",

@@ -23,9 +23,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DQDK_OFFLOAD_ARCH", "gfx950")
 REF = Path(os.environ.get("DQDK_REFERENCE", "/root/reference"))
 
-HIP_SRCS = ["rx_kernels.hip", "egress_kernels.hip", "membench.hip", "dqdk_gpu.hip"]
+HIP_SRCS = ["rx_kernels.hip", "egress_kernels.hip", "membench.hip", "dqdk_gpu.hip", "frame_processor.hip"]
 C_SRCS = ["synth.c"]
-HDRS = ["rx_kernels.h", "egress_kernels.h", str(ROOT / "include" / "dqdk_gpu.h")]
+HDRS = ["rx_kernels.h", "egress_kernels.h", "queue_internal.h", str(ROOT / "include" / "dqdk_gpu.h")]
 
 
 def _run(cmd: list[str]) -> None:

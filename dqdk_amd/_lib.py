@@ -46,6 +46,11 @@ class Cfg(C.Structure):
                 ("port_start", C.c_uint16), ("port_end", C.c_uint16)]
 
 
+class FpCfg(C.Structure):
+    _fields_ = [("cfg", Cfg), ("slot_payloads", C.c_uint32), ("nslots", C.c_uint32), ("device_first", C.c_int),
+                ("ndevices", C.c_int)]
+
+
 class SynthCfg(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("queue", C.c_uint32), ("frame_len", C.c_uint32),
                 ("stride", C.c_uint32), ("faulty", C.c_uint32)]
@@ -91,6 +96,11 @@ SIGNATURES = {
     "dqdk_gpu_histogram_accumulate": (C.c_int, [_P, _P]),
     "dqdk_gpu_histogram_reset": (C.c_int, [_P]),
     "dqdk_gpu_histogram_device_ptr": (_P, [_P]),
+    "dqdk_gpu_fp_init": (C.c_int, [C.POINTER(FpCfg)]),
+    "dqdk_gpu_fp_bind": (C.c_int, [_P, C.c_int, _P, C.c_uint64]),
+    "dqdk_gpu_frame_processor": (C.c_int, [_P, _P, C.c_uint32]),
+    "dqdk_gpu_fp_flush": (C.c_int, [_P]),
+    "dqdk_gpu_fp_fini": (C.c_int, [_P, C.c_int, C.POINTER(Counters)]),
     "dqdk_gpu_raw_compact_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, _P, C.c_uint64,
                                               C.POINTER(C.c_uint64)]),
     "dqdk_gpu_queue_set_raw_fd": (C.c_int, [_P, C.c_int]),

@@ -175,14 +175,18 @@ struct dqdk_gpu_queue {
     uint32_t* d_snap = nullptr;    // u32 snapshot for histogram_device_ptr (lazy)
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
-    uint32_t* d_keys = nullptr;
-    uint32_t* d_part1 = nullptr;   // partitioned-histogram staging (max_batch * E each)
+    uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
+    uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
+    uint64_t part1_elems = 0;
+    uint32_t* d_part1_rec = nullptr;  // records path: rx_part1's output when d_part1 is smaller (first use)
+    uint32_t* d_ovf = nullptr;     // fused path: the overflow list (ovf_blk_elems keys)
+    uint32_t ovf_cap_blk = 0;      // fused path: keys per block overflow region
     uint16_t* d_part2 = nullptr;
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
     uint32_t* d_fix = nullptr;     // fused path: decoded frames that failed afterwards (max_batch)
     uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions (in d_part1's rx_part1 region)
-    uint64_t ovf_blk_elems = 0;
+    uint64_t ovf_blk_elems = 0;    // grid * ovf_cap_blk
     uint64_t fused_elems = 0;      // fused path: pieces region (0: the fused path is off)
     uint64_t nk_max = 0;           // max_batch * E
     uint64_t scratch_words = 0;    // kHistScratchWords per staged slot
@@ -339,20 +343,104 @@ uint32_t fused_round_windows(uint32_t E)
     return std::max<uint32_t>(kFRingW, std::min<uint32_t>(64, wr));
 }
 
+// Records-path buffers, allocated on the first batch that takes that path
+// (the fused path, the benchmarked one, needs neither): frame-order keys
+// (unless the caller passes its own record buffer) and rx_part1's grouped
+// copy of them (d_part1 when it is large enough).
+int ensure_records(dqdk_gpu_queue* q, bool keys, bool part1)
+{
+    hipError_t e;
+    if (keys && !q->d_keys && (e = dev_alloc(&q->d_keys, q->nk_max * 4, q->alloc_kind)) != hipSuccess) {
+        q->d_keys = nullptr;
+        return (fail("hipMalloc(records)", e), -ENOMEM);
+    }
+    const uint64_t need = q->nk_max + kStagePad;
+    if (part1 && q->part1_elems < need && !q->d_part1_rec &&
+        (e = dev_alloc(&q->d_part1_rec, need * 4, q->alloc_kind)) != hipSuccess) {
+        q->d_part1_rec = nullptr;
+        return (fail("hipMalloc(records)", e), -ENOMEM);
+    }
+    return 0;
+}
+
+uint32_t* records_part1(const dqdk_gpu_queue* q)
+{
+    return q->part1_elems >= q->nk_max + kStagePad ? q->d_part1 : q->d_part1_rec;
+}
+
+// Histogram accumulation of a batch's keys (K3): frame-order records (the
+// atomic path, or rx_part1 -> rx_part2 on the partitioned one), or with fg
+// set the fused decode's pieces + overflow list.  The partitioned path stages
+// the batch for the slice pass (hist_k batches per pass).
+int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_res, const uint32_t* keys,
+                 bool partitioned, const FusedGeom* fg, const RxArgs& ra, uint32_t* slot_scratch)
+{
+    HistoArgs ha{};
+    ha.res = d_res;
+    ha.keys = keys;
+    ha.n = n;
+    ha.E = q->E;
+    ha.flags = q->cfg.flags;
+    ha.batch_scratch = q->d_batch;
+    ha.hist = q->d_hist;
+    ha.lo = q->d_lo;
+    ha.scratch = slot_scratch;
+    const bool fused = fg != nullptr;
+    ha.part1 = fused ? q->d_part1 : records_part1(q);
+    ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
+    ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
+    if (fused) {
+        ha.keys = q->d_ovf;                     // the overflow list
+        ha.total_keys = slot_scratch + kOffOvfN;
+        ha.part1_base = (uint64_t)kL1Buckets * fg->region;
+        ha.fused = 1;
+        ha.fgrid = fg->grid;
+        ha.piece_cap = fg->cap;
+        ha.piece_words = fg->words;
+        ha.region = fg->region;
+    }
+    if (!partitioned) {
+        const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
+        StageTimer t(q, kStAtomic);
+        hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    const uint64_t nkeys = (uint64_t)n * q->E;
+    const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
+    const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
+                                               (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
+    const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
+                                                (uint32_t)q->cu_count * 2u);
+    {
+        // fused: the decode's piece scans and checksum-failed frames,
+        // then the overflow list (usually empty), timed as "rx_fixup"
+        StageTimer t(q, fused ? kStFixup : kStPart1);
+        hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ra, ha);
+    }
+    {
+        StageTimer t(q, kStPart2);
+        // non-temporal key loads where the fused decode's are (fused_policy bit 1)
+        if (fused_policy(q->E) & 2u)
+            hipLaunchKernelGGL(rx_part2_kernel<2>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+        else
+            hipLaunchKernelGGL(rx_part2_kernel<0>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
+    }
+    HIPCHK(hipGetLastError());
+    if (++q->hist_pending == q->hist_k)
+        return hist_flush(q);
+    return 0;
+}
+
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
 {
-    uint32_t* keys = d_keys ? d_keys : q->d_keys;
-    if (q->histo && q->E && !keys)
-        return fail_errno(-EINVAL, "histogram mode needs a key buffer");
-
     RxArgs ra{};
     ra.umem = d_umem;
     ra.umem_size = umem_size;
     ra.desc = d_desc;
     ra.n = n;
     ra.res = d_res;
-    ra.keys = keys;
     ra.E = q->E;
     ra.flags = q->cfg.flags;
     ra.port_start = q->cfg.port_start;
@@ -368,6 +456,12 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     const bool fused = partitioned && !d_keys && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT) && q->d_fix &&
                        !(q->cfg.flags & DQDK_GPU_F_HISTO_UNFUSED) &&
                        (uint64_t)kL1Buckets * fg.region <= q->fused_elems;
+    if (!fused && q->histo && q->E) {
+        if (int rc = ensure_records(q, !d_keys, partitioned))
+            return rc;
+    }
+    uint32_t* keys = d_keys ? d_keys : q->d_keys;
+    ra.keys = keys;
     uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * q->scratch_words;
     ra.cnt1 = partitioned && !fused ? slot_scratch + kOffCnt1 : nullptr;
     if (partitioned)
@@ -380,14 +474,14 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.piece_cap = fg.cap;
         ra.piece_words = fg.words;
         ra.region = fg.region;
-        ra.ovf = q->d_keys;
+        ra.ovf = q->d_ovf;
         ra.fix = q->d_fix;
         ra.round_windows = fused_round_windows(q->E);
-        const uint32_t nsuper = (n + 64 * kFWaves - 1) / (64 * kFWaves);
         const uint32_t grid = fg.grid;
-        // private overflow regions: every key of a block's super-tiles fits its region
+        // private overflow regions of ovf_cap_blk keys (past them: the table)
         ra.ovf_blk = q->d_ovf_blk;
-        ra.ovf_blk_cap = (uint32_t)(((nsuper + grid - 1) / grid) * (uint64_t)(64 * kFWaves) * q->E);
+        ra.ovf_blk_cap = q->ovf_cap_blk;
+        ra.hist = q->d_hist;
         if ((uint64_t)ra.ovf_blk_cap * grid > q->ovf_blk_elems)
             return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
         StageTimer t(q, kStDecode);
@@ -429,62 +523,59 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     HIPCHK(hipGetLastError());
 
-    if (q->histo && q->E) {
-        HistoArgs ha{};
-        ha.res = d_res;
-        ha.keys = keys;
-        ha.n = n;
-        ha.E = q->E;
-        ha.flags = q->cfg.flags;
-        ha.batch_scratch = q->d_batch;
-        ha.hist = q->d_hist;
-        ha.lo = q->d_lo;
-        ha.scratch = slot_scratch;
-        ha.part1 = q->d_part1;
-        ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
-        ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
-        if (fused) {
-            ha.keys = q->d_keys;                    // the overflow list
-            ha.total_keys = slot_scratch + kOffOvfN;
-            ha.part1_base = (uint64_t)kL1Buckets * fg.region;
-            ha.fused = 1;
-            ha.fgrid = fg.grid;
-            ha.piece_cap = fg.cap;
-            ha.piece_words = fg.words;
-            ha.region = fg.region;
-        }
-        if (!partitioned) {
-            const uint32_t grid_h = std::min<uint32_t>((n + 3) / 4, (uint32_t)q->cu_count * 8u);
-            StageTimer t(q, kStAtomic);
-            hipLaunchKernelGGL(rx_histo_atomic_kernel, dim3(grid_h), dim3(256), 0, q->stream, ha);
-        } else {
-            const uint64_t nkeys = (uint64_t)n * q->E;
-            const uint32_t chunks = (uint32_t)((nkeys + kPartChunk - 1) / kPartChunk);
-            const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
-                                                       (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
-            const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
-                                                        (uint32_t)q->cu_count * 2u);
-            {
-                // fused: the decode's piece scans and checksum-failed frames,
-                // then the overflow list (usually empty), timed as "rx_fixup"
-                StageTimer t(q, fused ? kStFixup : kStPart1);
-                hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ra, ha);
-            }
-            {
-                StageTimer t(q, kStPart2);
-                // non-temporal key loads where the fused decode's are (fused_policy bit 1)
-                if (fused_policy(q->E) & 2u)
-                    hipLaunchKernelGGL(rx_part2_kernel<2>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
-                else
-                    hipLaunchKernelGGL(rx_part2_kernel<0>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
-            }
-            HIPCHK(hipGetLastError());
-            if (++q->hist_pending == q->hist_k)
-                return hist_flush(q);
-        }
-        HIPCHK(hipGetLastError());
-    }
+    if (q->histo && q->E)
+        return launch_histo(q, n, d_res, keys, partitioned, fused ? &fg : nullptr, ra, slot_scratch);
     return 0;
+}
+
+// The frame-processor plugin's batch (frame_processor.hip): n staged
+// payloads of E * 16 bytes at d_stage (DEVICE), their datalens at d_len.
+// fp_decode -> rx_count -> the records-path histogram, on the queue stream.
+int launch_payloads(dqdk_gpu_queue* q, const uint8_t* d_stage, const uint32_t* d_len, uint32_t n)
+{
+    const bool histo = q->histo && q->E;
+    const bool partitioned = histo && use_partitioned(q, n);
+    uint32_t* slot_scratch =
+        q->d_hscratch ? q->d_hscratch + (size_t)q->hist_pending * q->scratch_words : nullptr;
+    if (partitioned)
+        HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+    if (histo) {
+        if (int rc = ensure_records(q, true, partitioned))
+            return rc;
+    }
+    PayloadArgs pa{};
+    pa.stage = d_stage;
+    pa.len = d_len;
+    pa.n = n;
+    pa.E = q->E;
+    pa.histo = histo;
+    pa.res = q->d_res;
+    pa.keys = histo ? q->d_keys : nullptr;
+    pa.cnt1 = partitioned ? slot_scratch + kOffCnt1 : nullptr;
+    pa.batch_scratch = q->d_batch;
+    {
+        StageTimer t(q, kStDecode);
+        const uint32_t grid = std::min<uint32_t>((n + kWaves - 1) / kWaves, (uint32_t)q->cu_count * 8u);
+        hipLaunchKernelGGL(fp_decode_kernel, dim3(grid), dim3(kTile), 0, q->stream, pa);
+    }
+    CountArgs ca{};
+    ca.res = q->d_res;
+    ca.n = n;
+    ca.E = q->E;
+    ca.flags = q->cfg.flags;  // (no batch abort: the caller's fetch_xsk accounts its batches)
+    ca.histo = q->histo;
+    ca.batch_scratch = q->d_batch;
+    ca.cum = q->d_cum;
+    {
+        StageTimer t(q, kStCount);
+        const uint32_t grid_c = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count);
+        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_c), dim3(256), 0, q->stream, ca);
+    }
+    HIPCHK(hipGetLastError());
+    if (!histo)
+        return 0;
+    RxArgs ra{};  // (read by rx_part1 on the fused path only)
+    return launch_histo(q, n, q->d_res, q->d_keys, partitioned, nullptr, ra, slot_scratch);
 }
 
 // u32 view of table bins [first, first + nbins) (multiples of 16) into d_out, async.
@@ -640,6 +731,29 @@ int write_raw_sync(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size,
 
 }  // namespace
 
+// ---- runtime-internal entry points (queue_internal.h) -----------------------
+namespace dqdk {
+
+int queue_launch_payloads(dqdk_gpu_queue_t* q, const uint8_t* d_stage, const uint32_t* d_len, uint32_t n)
+{
+    if (!q || n > q->max_batch || (n && !d_len) || (n && q->histo && q->E && !d_stage))
+        return fail_errno(-EINVAL, "launch_payloads: bad argument");
+    if (n == 0)
+        return 0;
+    SETDEV(q->device);
+    return launch_payloads(q, d_stage, d_len, n);
+}
+
+int queue_device(const dqdk_gpu_queue_t* q) { return q ? q->device : -1; }
+
+uint32_t queue_events(const dqdk_gpu_queue_t* q) { return q && q->histo ? q->E : 0u; }
+
+int set_error(int err, const char* what) { return fail_errno(err, what); }
+
+int set_hip_error(const char* what, hipError_t e) { return fail(what, e); }
+
+}  // namespace dqdk
+
 extern "C" {
 
 int dqdk_gpu_abi_version(void) { return DQDK_GPU_ABI_VERSION; }
@@ -727,38 +841,71 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             // part2: item i of a staged batch at [i * kPartChunk, + keys)
             q->part2_stride = (size_t)max_items(nk) * kPartChunk;
             q->runs_stride = ((size_t)max_items(nk) * kItemOffs + 7) & ~(size_t)7;
-            // Stage up to kHistKMax batches per slice pass (the low-byte sweep
-            // of a touched slice is amortised over them; the pass drains its
-            // packed-u16 bins between groups of events, so any count of
-            // events per slice fits), as many as the staging budget holds;
-            // DQDK_GPU_F_HISTO_EAGER: a pass per batch.
-            const size_t slot_bytes = q->part2_stride * 2 + q->runs_stride * 2 + q->scratch_words * 4;
-            q->hist_k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
-                            ? 1u
-                            : (uint32_t)std::max<size_t>(
-                                  1, std::min(kHistKMax, kHistStageBytes / slot_bytes));
-            // fused decode's per-block overflow regions: grid * ceil(super-tiles / grid) super-tiles
+            // fused decode's per-block overflow regions: ovf_cap_blk keys each
+            // (an eighth of a block's keys, at least 64K: the 9000 B batches
+            // overflow ~3 % of their keys, 1500 B ones far fewer); past that
+            // a key is added to the table by a device atomic (exact, rare)
             const FusedGeom fg = fused_geom(max_batch, q->E, (uint64_t)q->dec_cus);
             const uint64_t nsuper = ((uint64_t)max_batch + 64 * kFWaves - 1) / (64 * kFWaves);
-            q->ovf_blk_elems = fg.grid * ((nsuper + fg.grid - 1) / fg.grid) * (64 * kFWaves) * q->E;
-            // part1 holds the fused decode's pieces, then rx_part1's region
-            // (records / overflow), which also backs the decode's overflow
-            // regions (dead before rx_part1 writes it); the fused pieces at
-            // max_batch bound those of any smaller batch; gathered items
-            // address them in 32-bit byte offsets per bucket
+            const uint64_t blk_keys = ((nsuper + fg.grid - 1) / fg.grid) * (64 * kFWaves) * q->E;
+            uint64_t ocap = std::min<uint64_t>(blk_keys, std::max<uint64_t>(65536, blk_keys / 8));
+            if (const char* v = getenv("DQDK_GPU_OVF_BLK"))  // (test hook: forces the atomic spill)
+                ocap = std::min<uint64_t>(blk_keys, std::max<uint64_t>(64, strtoull(v, nullptr, 0)));
+            q->ovf_cap_blk = (uint32_t)ocap;
+            q->ovf_blk_elems = (uint64_t)fg.grid * ocap;
+            // part1 holds the fused decode's pieces, then rx_part1's grouped
+            // copy of the overflow list, which also backs the decode's
+            // overflow regions (dead before rx_part1 writes it); the fused
+            // pieces at max_batch bound those of any smaller batch; gathered
+            // items address them in 32-bit byte offsets per bucket.  The
+            // records path (frame-order keys) allocates its buffers on first
+            // use (ensure_records): the fused path needs neither.
             q->fused_elems = fg.region * 4u < (1ull << 31) && (uint64_t)kL1Buckets * fg.region < (1ull << 32)
                                  ? (uint64_t)kL1Buckets * fg.region
                                  : 0u;
-            const size_t pe = (size_t)std::max<uint64_t>(part_elems(nk, q->fused_elems),
-                                                         q->fused_elems + q->ovf_blk_elems);
-            if ((e = dev_alloc(&q->d_keys, nk * 4, q->alloc_kind)) != hipSuccess ||
-                (e = dev_alloc(&q->d_part1, pe * 4, q->alloc_kind)) != hipSuccess ||
-                (e = dev_alloc(&q->d_part2, q->hist_k * q->part2_stride * 2, q->alloc_kind)) != hipSuccess ||
-                (e = dev_alloc(&q->d_runs, q->hist_k * q->runs_stride * sizeof(uint16_t), q->alloc_kind)) != hipSuccess ||
-                (e = dev_alloc(&q->d_hscratch, q->hist_k * q->scratch_words * sizeof(uint32_t), q->alloc_kind)) != hipSuccess ||
-                (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
-                return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
-            q->d_ovf_blk = q->d_part1 + q->fused_elems;
+            if (q->fused_elems) {
+                q->part1_elems = q->fused_elems + q->ovf_blk_elems + kStagePad;
+                if ((e = dev_alloc(&q->d_part1, q->part1_elems * 4, q->alloc_kind)) != hipSuccess ||
+                    (e = hipMalloc(&q->d_ovf, q->ovf_blk_elems * sizeof(uint32_t))) != hipSuccess ||
+                    (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
+                    return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
+                q->d_ovf_blk = q->d_part1 + q->fused_elems;
+            }
+            if (cfg->flags & (DQDK_GPU_F_BATCH_ABORT | DQDK_GPU_F_HISTO_UNFUSED)) {
+                if (int rc = ensure_records(q, true, true))  // records path every batch
+                    return cleanup(rc);
+            }
+            // Stage up to kHistKMax batches per slice pass (the low-byte sweep
+            // of a touched slice is amortised over them; the pass drains its
+            // packed-u16 bins between groups of events, so any count of
+            // events per slice fits), as many as the staging budget holds:
+            // 24 GiB, or a quarter of the device memory still free (ADVICE r3:
+            // several queues per GPU), halved while an allocation fails;
+            // DQDK_GPU_F_HISTO_EAGER: a pass per batch.
+            const size_t slot_bytes = q->part2_stride * 2 + q->runs_stride * 2 + q->scratch_words * 4;
+            size_t budget = kHistStageBytes;
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 4 < budget)
+                budget = free_b / 4;
+            uint32_t k = (cfg->flags & DQDK_GPU_F_HISTO_EAGER)
+                             ? 1u
+                             : (uint32_t)std::max<size_t>(1, std::min(kHistKMax, budget / slot_bytes));
+            for (;; k /= 2) {
+                if ((e = dev_alloc(&q->d_part2, k * q->part2_stride * 2, q->alloc_kind)) == hipSuccess &&
+                    (e = dev_alloc(&q->d_runs, k * q->runs_stride * sizeof(uint16_t), q->alloc_kind)) == hipSuccess &&
+                    (e = dev_alloc(&q->d_hscratch, k * q->scratch_words * sizeof(uint32_t), q->alloc_kind)) == hipSuccess)
+                    break;
+                (void)hipGetLastError();
+                dev_free(q->d_part2);
+                dev_free(q->d_runs);
+                dev_free(q->d_hscratch);
+                q->d_part2 = nullptr;
+                q->d_runs = nullptr;
+                q->d_hscratch = nullptr;
+                if (k == 1)
+                    return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
+            }
+            q->hist_k = k;
         }
     }
     *out = q;
@@ -780,7 +927,7 @@ int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out)
     if (e != hipSuccess)
         return (fail("device_alloc", e), -ENOMEM);
     *d_out = p;
-    return got == want ? 0 : 1;
+    return got == kAllocContig ? 0 : 1;  // 0 only for a physically contiguous range
 }
 
 int dqdk_gpu_device_free(int device, void* d_ptr)
@@ -818,6 +965,8 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_batch);
     dev_free(q->d_keys);
     dev_free(q->d_part1);
+    dev_free(q->d_part1_rec);
+    (void)hipFree(q->d_ovf);
     dev_free(q->d_part2);
     dev_free(q->d_runs);
     dev_free(q->d_hscratch);
@@ -956,68 +1105,87 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
     }
     const uint8_t* dev_umem = (const uint8_t*)reg->dev + (umem - (const uint8_t*)reg->host);
     HIPCHK(hipMemcpyAsync(q->d_desc, d, (size_t)n * sizeof(*d), hipMemcpyHostToDevice, q->stream));
+    // Once the batch is enqueued, no path returns before the queue stream has
+    // drained: its kernels read the caller's frames (valid only until this
+    // call returns, src/dqdk.c:300) and its copies land in per_pkt and in this
+    // frame's b[].
+    auto drained = [&](int err) {
+        const hipError_t e = hipStreamSynchronize(q->stream);
+        return err ? err : e != hipSuccess ? fail("hipStreamSynchronize", e) : 0;
+    };
     int rc = launch_batch(q, dev_umem, umem_size, q->d_desc, n, q->d_res, nullptr);
     if (rc)
-        return rc;
+        return drained(rc);
     const bool raw = q->raw_fd >= 0 && !q->raw_sync;
     const int k = (int)(q->raw_seq & 1);
     uint64_t cap = 0;
+    hipError_t e = hipSuccess;
     if (raw) {
         // the batch's raw stream (tristan.c:318-324) is gathered into buffer k
         // now (the frames are valid only until this call returns, dqdk.c:300);
         // capacity: the frames' bytes (a payload lies inside its frame unless
         // its datalen wrapped, handled below by a second gather)
         if (!q->raw_stream) {
-            HIPCHK(hipStreamCreateWithFlags(&q->raw_stream, hipStreamNonBlocking));
-            for (int j = 0; j < 2; j++)
-                HIPCHK(hipEventCreateWithFlags(&q->raw_ev_d2h[j], hipEventDisableTiming));
-            HIPCHK(hipHostMalloc(&q->h_raw_total, sizeof(uint64_t), hipHostMallocDefault));
+            if ((e = hipStreamCreateWithFlags(&q->raw_stream, hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&q->raw_ev_d2h[0], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&q->raw_ev_d2h[1], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipHostMalloc(&q->h_raw_total, sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
+                return drained(fail("raw egress setup", e));
         }
         uint64_t guess = 0;
         for (uint32_t i = 0; i < n; i++)
             guess += d[i].len;
         if ((rc = grow_dev(&q->d_rawb[k], &q->d_rawb_cap[k], std::max<uint64_t>(guess, 4096))) != 0)
-            return rc;
+            return drained(rc);
         cap = q->d_rawb_cap[k];
         if ((rc = launch_raw(q, dev_umem, umem_size, q->d_desc, n, q->d_res, q->d_rawb[k], cap, true)) != 0)
-            return rc;
+            return drained(rc);
         const uint32_t nblk = (n + kRawThreads - 1) / kRawThreads;
-        HIPCHK(hipMemcpyAsync(q->h_raw_total, q->d_raw_blk + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                              q->stream));
+        if ((e = hipMemcpyAsync(q->h_raw_total, q->d_raw_blk + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                q->stream)) != hipSuccess)
+            return drained(fail("hipMemcpyAsync", e));
     } else if (q->raw_fd >= 0 && (rc = write_raw_sync(q, dev_umem, umem_size, n)) != 0) {
-        return rc;
+        return drained(rc);
     }
-    HIPCHK(hipMemcpyAsync(per_pkt, q->d_res, (size_t)n * sizeof(*per_pkt), hipMemcpyDeviceToHost, q->stream));
     uint64_t b[kBatchScratch];
-    HIPCHK(hipMemcpyAsync(b, q->d_batch, sizeof(b), hipMemcpyDeviceToHost, q->stream));
-    // the previous batch's raw stream goes to its file while this batch runs
-    if (raw && (rc = raw_write_pending(q, k ^ 1)) != 0)
+    if ((e = hipMemcpyAsync(per_pkt, q->d_res, (size_t)n * sizeof(*per_pkt), hipMemcpyDeviceToHost, q->stream)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(b, q->d_batch, sizeof(b), hipMemcpyDeviceToHost, q->stream)) != hipSuccess)
+        return drained(fail("hipMemcpyAsync", e));
+    // the previous batch's raw stream goes to its file while this batch runs;
+    // a failed write() is returned after this batch is complete (its own raw
+    // stream still queued for the next write)
+    const int werr = raw ? raw_write_pending(q, k ^ 1) : 0;
+    if ((rc = drained(0)) != 0)
         return rc;
-    HIPCHK(hipStreamSynchronize(q->stream));
     if (delta)
         memcpy(delta, &b[1], sizeof(*delta));
     if (raw) {
         const uint64_t total = *q->h_raw_total;
         if (total > cap) {  // wrapped datalen inside the UMEM: gather again at full size
-            if ((rc = grow_dev(&q->d_rawb[k], &q->d_rawb_cap[k], total)) != 0 ||
+            // (capacity grows geometrically and is kept: batches with such
+            // frames reallocate rarely)
+            if ((rc = grow_dev(&q->d_rawb[k], &q->d_rawb_cap[k], std::max(total, 2 * cap))) != 0 ||
                 (rc = launch_raw(q, dev_umem, umem_size, q->d_desc, n, q->d_res, q->d_rawb[k], total, true)) != 0)
-                return rc;
+                return drained(rc);
         }
         if (total) {
             if ((rc = grow_host(&q->h_rawb[k], &q->h_rawb_cap[k], total)) != 0)
-                return rc;
-            HIPCHK(hipEventRecord(q->raw_ev_d2h[k], q->stream));  // after the gather
-            HIPCHK(hipStreamWaitEvent(q->raw_stream, q->raw_ev_d2h[k], 0));
-            HIPCHK(hipMemcpyAsync(q->h_rawb[k], q->d_rawb[k], total, hipMemcpyDeviceToHost, q->raw_stream));
-            HIPCHK(hipEventRecord(q->raw_ev_d2h[k], q->raw_stream));
+                return drained(rc);
+            if ((e = hipEventRecord(q->raw_ev_d2h[k], q->stream)) != hipSuccess ||  // after the gather
+                (e = hipStreamWaitEvent(q->raw_stream, q->raw_ev_d2h[k], 0)) != hipSuccess ||
+                (e = hipMemcpyAsync(q->h_rawb[k], q->d_rawb[k], total, hipMemcpyDeviceToHost, q->raw_stream)) !=
+                    hipSuccess ||
+                (e = hipEventRecord(q->raw_ev_d2h[k], q->raw_stream)) != hipSuccess)
+                return drained(fail("raw egress D2H", e));
             q->raw_pend[k] = 1;
             q->raw_pend_len[k] = total;
         }
-        if (total > cap)  // the second gather read the frames: done before returning
-            HIPCHK(hipStreamSynchronize(q->stream));
         q->raw_seq++;
+        if (total > cap && (rc = drained(0)) != 0)  // the second gather read the frames: done before returning
+            return rc;
     }
-    return 0;
+    return werr;
 }
 
 int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out)

@@ -171,9 +171,10 @@ struct RxArgs {
     uint32_t piece_cap;
     uint32_t piece_words;
     uint64_t region;          // u32 words per bucket (fused_geom)
-    uint32_t* ovf;            // overflow list (n*E keys)
+    uint32_t* ovf;            // overflow list (gridDim.x * ovf_blk_cap keys)
     uint32_t* ovf_blk;        // per-block private overflow regions (gridDim.x * ovf_blk_cap keys)
-    uint32_t ovf_blk_cap;
+    uint32_t ovf_blk_cap;     // keys per region; past it (pathological spectra) a key is added to
+    uint32_t* hist;           //   the table's base plane by a device atomic (exact: value = base + low)
     uint32_t* fix;            // decoded frames whose final status is not OK (n)
     uint32_t round_windows;   // windows per wave per round (multiple of the ring depth)
 };
@@ -216,7 +217,25 @@ struct HistoArgs {
     uint64_t part2_stride, runs_stride;
 };
 
+// Frame-processor plugin (dqdk_gpu_frame_processor, frame_processor.hip):
+// the payloads of n tristan_process(payload, datalen, 1) calls
+// (src/tristan.c:308-330, via process_unbuffered_frame :377-381), staged back
+// to back: payload p's E events at stage + p * E * 16 (the bytes
+// process_events_unrolled16 reads, :247-304), its datalen at len[p].
+struct PayloadArgs {
+    const uint8_t* stage;
+    const uint32_t* len;
+    uint32_t n;
+    uint32_t E;
+    int histo;                // decode events (is_store_histo, src/tristan.c:65-70)
+    dqdk_gpu_rx_result_t* res;  // per call: {datalen, OK, 0, rejected events}
+    uint32_t* keys;           // n * E frame-order records (DQDK_KEY_NONE: rejected)
+    uint32_t* cnt1;           // partitioned histogram: keys per L1 bucket, or null
+    uint64_t* batch_scratch;  // per-batch state (reset here, read by rx_count)
+};
+
 __global__ void rx_decode_kernel(RxArgs a);
+__global__ void fp_decode_kernel(PayloadArgs a);
 template <int kLdAux, bool kLines>
 __global__ void rx_decode_fused_kernel(RxArgs a);
 __global__ void rx_abort_kernel(CountArgs a);

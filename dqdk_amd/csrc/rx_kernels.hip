@@ -774,6 +774,66 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
 }
 
 // ===========================================================================
+// Frame-processor plugin: payloads staged by dqdk_gpu_frame_processor, one
+// per tristan_process(payload, datalen, 1) call (src/tristan.c:308-330).  A
+// wave takes one payload at a time: lane e decodes events e, e + 64, ...
+// (16-B aligned loads: the staging stride is E * 16) into frame-order
+// records, exactly histogram_event's key and bounds (src/tristan.c:233-245);
+// lane 0 writes the call's result record (datalen, rejected events) for
+// rx_count.  The records feed the records-path histogram (atomic or
+// partitioned), as rx_decode's do.
+// ===========================================================================
+__global__ void __launch_bounds__(kTile) fp_decode_kernel(PayloadArgs a)
+{
+    __shared__ uint32_t cnt[kL1Buckets];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    if (a.cnt1) {
+        for (int b = tid; b < kL1Buckets; b += kTile)
+            cnt[b] = 0;
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && tid < 17)
+        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
+    const uint32_t gw = (blockIdx.x * kTile + (uint32_t)tid) >> 6;
+    const uint32_t nw = (gridDim.x * kTile) >> 6;
+    for (uint32_t p = gw; p < a.n; p += nw) {
+        uint32_t oob = 0;
+        if (a.histo) {
+            const u32x4* ev = (const u32x4*)(a.stage + (uint64_t)p * a.E * 16u);
+            uint32_t* k = a.keys + (uint64_t)p * a.E;
+            for (uint32_t e = (uint32_t)lane; e < a.E; e += 64) {
+                const u32x4 v = __builtin_nontemporal_load(&ev[e]);
+                const uint32_t ch = v.x >> 16;             // event bytes 2..3
+                const uint32_t bin = (v.y >> 8) & 0xffffu;  // event bytes 5,6 = energy >> 8
+                const uint32_t hc = v.z & 7u;               // byte 8, hist_class:3
+                const bool inb = ch < kChannels && hc < kHists;
+                const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;
+                k[e] = inb ? key : DQDK_KEY_NONE;
+                oob += inb ? 0u : 1u;
+                if (inb && a.cnt1)
+                    atomicAdd(&cnt[key >> kL1Shift], 1u);
+            }
+            oob = wave_sum_dpp(oob);
+        }
+        if (lane == 0) {
+            dqdk_gpu_rx_result_t r;
+            r.datalen = a.len[p];
+            r.status = DQDK_RX_OK;  // process_frame calls the processor only for datalen != 0
+            r.payload_off = 0;
+            r.oob_events = (uint16_t)oob;  // E <= 65535
+            a.res[p] = r;
+        }
+    }
+    if (a.cnt1) {
+        __syncthreads();
+        for (int b = tid; b < kL1Buckets; b += kTile)
+            if (cnt[b])
+                atomicAdd(&a.cnt1[b], cnt[b]);
+    }
+}
+
+// ===========================================================================
 // Fused decode: rx_decode + rx_part1 in one persistent kernel.  A block of
 // kFWaves waves takes kFWaves 64-frame tiles at a time (a super-tile); its
 // waves stream their frames exactly as rx_decode does, but a decoded key goes
@@ -804,6 +864,21 @@ struct FusedLds {
 // lgkmcnt(0) (this wave's LDS operations performed) is enough.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// A key for the block's private overflow region at `slot` (valid lanes only):
+// the region holds ovf_blk_cap keys; past that (a pathological spectrum) the
+// key goes straight to the table's base plane by a relaxed device atomic --
+// the reference's ++ (src/tristan.c:243); exact, since a bin's value is base
+// + low (mod 2^32).  The store is issued by every lane (dropped at kOOB), the
+// atomic only in this rare branch.
+__device__ __forceinline__ void ovf_put(const RxArgs& a, __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t key, bool valid,
+                                        uint32_t slot)
+{
+    const bool fits = valid && slot < a.ovf_blk_cap;
+    __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, fits ? 4u * slot : kOOB, 0, 0);
+    if (valid && !fits)
+        __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One event per 16-B chunk (as decode_chunk): the key goes to the LDS stage
 // of its bucket; past kFCap staged keys (rare) it goes to the block's private
 // overflow region.  The overflow store is issued by every lane of every
@@ -811,8 +886,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // from an LDS counter: the window loop's VMEM pattern stays fixed, so the
 // compiler waits for ring loads with vmcnt(N) instead of draining the ring (a
 // conditional global atomic or store here would force near-full waits).
-__device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef, uint32_t oob_slot,
-                                            FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc)
+__device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef,
+                                            uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc)
 {
     const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
     const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
@@ -838,7 +913,6 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
 
     // overflow slots: one LDS atomic per wave (lanes ranked by mbcnt), not one
     // per key on the block's single counter (64 lanes on one address serialise)
-    uint32_t ooff = kOOB;
     const uint64_t om = __ballot(ov);
     if (om) {
         const uint32_t first = (uint32_t)__builtin_ctzll(om);
@@ -846,11 +920,11 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
         if ((uint32_t)(threadIdx.x & 63) == first)
             base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
         base = rdl(base, first);
-        if (ov)
-            ooff = 4u * (base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
+        ovf_put(a, ovf_rsrc, key, ov,
+                base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, kOOB, 0, 0);
     }
-    __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, ooff, 0, 0);
 }
 
 // Both chunks of a window at once, without divergent branches: every lane
@@ -867,9 +941,9 @@ __device__ __forceinline__ void fused_chunk(const u32x4& v, uint32_t r, uint32_t
 // Stage counts (and per-frame out-of-bounds counts) step by kCntUnit: with 4
 // a count is the byte offset of the slot, so a stage address is one mad.
 constexpr uint32_t kCntUnit = DQDK_FPAIR >= 2 ? 4u : 1u;
-__device__ __forceinline__ void fused_pair(const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0, uint32_t Ef,
-                                           uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc,
-                                           uint32_t lane)
+__device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0,
+                                           uint32_t Ef, uint32_t oob_slot, FusedLds& lds,
+                                           __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane)
 {
     uint32_t key[2], b[2];
     uint32_t* cnt[2];
@@ -921,8 +995,8 @@ __device__ __forceinline__ void fused_pair(const u32x4& va, const u32x4& vb, uin
         base = rdl(base, first);
         const uint32_t r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
         const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-        __builtin_amdgcn_raw_buffer_store_b32(key[0], ovf_rsrc, ov0 ? 4u * (base + r0) : kOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(key[1], ovf_rsrc, ov1 ? 4u * (base + n0 + r1) : kOOB, 0, 0);
+        ovf_put(a, ovf_rsrc, key[0], ov0, base + r0);
+        ovf_put(a, ovf_rsrc, key[1], ov1, base + n0 + r1);
     }
 }
 
@@ -1001,7 +1075,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
             o = atomicAdd(&lds.ovf_n, nov);
         o = rfl(o);
         for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
-            __builtin_amdgcn_raw_buffer_store_b32(lds.stage[bj * kFCap + fj + t], ovf_rsrc, 4u * (o + t), 0, 0);
+            ovf_put(a, ovf_rsrc, lds.stage[bj * kFCap + fj + t], true, o + t);
     }
     // carry the remainders to the stage's start (fewer keys than were
     // flushed, so source and destination do not overlap)
@@ -1048,7 +1122,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     if (tid == 0)
         lds.ovf_n = 0;
     __syncthreads();
-    // this block's private overflow region: room for every key of its super-tiles
+    // this block's private overflow region (ovf_blk_cap keys, then the table)
     uint32_t* const ovf_blk = a.ovf_blk + (uint64_t)blockIdx.x * a.ovf_blk_cap;
     const __amdgpu_buffer_rsrc_t ovf_rsrc = uniform_rsrc(ovf_blk, (uint64_t)a.ovf_blk_cap * 4u);
     if (blockIdx.x == 0 && tid < 17)
@@ -1137,10 +1211,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
 #if DQDK_FPAIR
-                fused_pair(b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
+                fused_pair(a, b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
 #else
-                fused_chunk(b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
-                fused_chunk(b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
+                fused_chunk(a, b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
+                fused_chunk(a, b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
 #endif
                 if (active && ++wp == P.nwin) {
                     frame_sum_add(&lds.sum[wslot0 + jp], &lds.stage[kL1Buckets * kFCap + lane], acc0 + acc1,
@@ -1188,7 +1262,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     __syncthreads();  // (also orders the region's stores before the copy below)
     // (the last flush left every stage count at 0: they count the region's
     // keys per bucket here, then one device atomic per bucket per block)
-    const uint32_t nov = lds.ovf_n;
+    const uint32_t nov = min(lds.ovf_n, a.ovf_blk_cap);  // (the keys past the region went to the table)
     if (nov) {
         if (tid == 0)
             lds.wtot[0] = atomicAdd(&a.scratch[kOffOvfN], nov);

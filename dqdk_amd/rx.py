@@ -234,6 +234,60 @@ class RxQueue:
                 if nm and not nm.startswith(b"(")}  # "(unused)" stage slots
 
 
+class FrameProcessor:
+    """DQDK's frame-processor plugin on the GPU: ``dqdk_gpu_frame_processor``
+    is a ``dqdk_frame_processor_t`` (src/dqdk.h:84-85) that the unmodified
+    receive loop calls once per valid payload (process_frame,
+    src/dqdk.c:231-250), standing in for process_unbuffered_frame
+    (src/tristan.c:377-381).  Workers are any distinct addresses (the
+    reference's dqdk_worker_t pointers); one GPU queue per worker.
+
+    ``fn_ptr`` is the C function pointer to register as ``proc`` in
+    dqdk_ctx_init (src/tristan.c:589-590); ``__call__`` calls it from Python.
+    """
+
+    def __init__(self, cfg: RxConfig, slot_payloads: int = 0, nslots: int = 0, device_first: int = 0,
+                 ndevices: int = 0):
+        self.cfg = cfg
+        c = L.FpCfg(cfg.to_c(), slot_payloads, nslots, device_first, ndevices)
+        L.check(L.lib().dqdk_gpu_fp_init(C.byref(c)), "dqdk_gpu_fp_init")
+        self._open = True
+
+    @property
+    def fn_ptr(self) -> int:
+        return C.cast(L.lib().dqdk_gpu_frame_processor, C.c_void_p).value
+
+    def bind(self, worker: int, device: int = -1, umem: np.ndarray | None = None) -> None:
+        """Give the worker its GPU (and UMEM bound) before its first frame."""
+        L.check(L.lib().dqdk_gpu_fp_bind(worker, device, umem.ctypes.data if umem is not None else None,
+                                         umem.nbytes if umem is not None else 0), "dqdk_gpu_fp_bind")
+
+    def __call__(self, worker: int, data_ptr: int, datalen: int) -> int:
+        """One tristan_process(data, datalen, 1) call; returns 0 or -errno like the reference."""
+        return L.lib().dqdk_gpu_frame_processor(worker, data_ptr, datalen)
+
+    def flush(self, worker: int) -> None:
+        L.check(L.lib().dqdk_gpu_fp_flush(worker), "dqdk_gpu_fp_flush")
+
+    def fini(self, host_hist: np.ndarray | None = None, csv_fd: int = -1) -> dict:
+        """Drain every worker; add their tables into host_hist (tristan_t::histo),
+        write the merged CSV to csv_fd; return the summed counters."""
+        if host_hist is not None:
+            assert host_hist.dtype == np.uint32 and host_hist.size == L.HISTO_ENTRIES and host_hist.flags.c_contiguous
+        tot = L.Counters()
+        self._open = False
+        L.check(L.lib().dqdk_gpu_fp_fini(host_hist.ctypes.data if host_hist is not None else None, csv_fd,
+                                         C.byref(tot)), "dqdk_gpu_fp_fini")
+        return tot.as_dict()
+
+    def __del__(self):
+        if getattr(self, "_open", False):
+            try:
+                L.lib().dqdk_gpu_fp_fini(None, -1, None)
+            except Exception:
+                pass
+
+
 def tristan_summary(counters: list[dict], runtime_ns: list[int] | None = None, directory: str = "") -> str:
     """tristan_fini's controller status line (src/tristan.c:171-189) via the C ABI."""
     objs = [L.Counters(**{f: int(c.get(f, 0)) for f in L.COUNTER_FIELDS}) for c in counters]

@@ -179,6 +179,62 @@ int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
 int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,
                       uint32_t n, dqdk_gpu_rx_result_t* per_pkt, dqdk_gpu_counters_t* delta);
 
+/* ---- frame-processor plugin (dqdk_frame_processor_t, src/dqdk.h:84-85) ---- */
+/* The reference's own operator API for this path: process_frame
+ * (src/dqdk.c:231-250) calls worker->frame_processor(worker, payload,
+ * datalen) once per frame whose get_udp_payload succeeded with datalen != 0,
+ * on that worker's pthread; TRISTAN registers process_unbuffered_frame
+ * (src/tristan.c:377-381, at :589-590), i.e. tristan_process(payload,
+ * datalen, 1) (:308-330): the E = payloadsz/16 events at the payload into
+ * the shared histogram, total_bytes += datalen, total_events += E, return 0.
+ *
+ * dqdk_gpu_frame_processor has exactly that signature and result, so an
+ * unmodified dqdk.c drives the GPU: register it as `proc` in dqdk_ctx_init
+ * (src/tristan.c:589-590) after dqdk_gpu_fp_init, and call dqdk_gpu_fp_fini
+ * before tristan_fini.  Per worker -- keyed by the worker
+ * pointer, never by worker->private (the shared tristan_t) -- each call
+ * copies the E * 16 bytes tristan_process reads (the copy post_async makes
+ * into its ring, src/dqdk.c:220-229) into a pinned staging slot and returns
+ * 0; a full slot is copied to the worker's GPU and decoded there
+ * asynchronously (the worker reuses the slot once that copy has landed).
+ * Returns 0, or -EIO / -ENOMEM / -ENODEV once the worker's GPU queue has
+ * failed (process_frame then aborts the batch like any processor error). */
+struct dqdk_worker; /* the reference's dqdk_worker_t (src/dqdk.h:87-105), opaque here */
+
+typedef struct dqdk_gpu_fp_cfg {
+    dqdk_gpu_cfg_t cfg;     /* payloadsz / mode as -s / -m; flags: histogram strategy only
+                               (the header checks stay in the caller's get_udp_payload) */
+    uint32_t slot_payloads; /* calls staged per GPU batch (0: 8192)                        */
+    uint32_t nslots;        /* pinned staging slots per worker, >= 2 (0: 4)                */
+    int device_first;       /* workers are spread round robin over devices                */
+    int ndevices;           /*   [device_first, device_first + ndevices) (0: all devices)   */
+} dqdk_gpu_fp_cfg_t;
+
+/* Before the workers start (tristan_init's place).  -EBUSY if already set up. */
+int dqdk_gpu_fp_init(const dqdk_gpu_fp_cfg_t* cfg);
+/* Optional, before the worker's first frame (e.g. after dqdk_ctx_init): give
+ * the worker its GPU now (device < 0: round robin) instead of at its first
+ * call, and its UMEM (nullable): event bytes a call would read at or past
+ * umem + umem_size are then taken as zeros, as the batch entry points do. */
+int dqdk_gpu_fp_bind(struct dqdk_worker* worker, int device, const void* umem, uint64_t umem_size);
+/* The dqdk_frame_processor_t (src/dqdk.h:85). */
+int dqdk_gpu_frame_processor(struct dqdk_worker* worker, uint8_t* data, uint32_t datalen);
+/* Optional: hand the worker's partly filled slot to the GPU now (e.g. when
+ * its RX ring runs empty).  Call on the worker's thread or after it stopped. */
+int dqdk_gpu_fp_flush(struct dqdk_worker* worker);
+/* After the workers have stopped (dqdk_waitall), before tristan_fini: every
+ * worker's staged calls are decoded, then
+ *   host_hist (nullable): every worker's table added (u32 wrap) into it --
+ *     tristan_t::histo, so tristan_fini's own CSV loop (:197-216) and JSON
+ *     summary run unchanged;
+ *   csv_fd >= 0: the merged table written as tristan_fini's CSV, formatted
+ *     on the GPU (dqdk_gpu_histogram_write_csv);
+ *   totals (nullable): the workers' counters summed -- total_events /
+ *     total_bytes are what tristan_process added to tristan_t (:327-328),
+ *     rcvd_pkts the calls, oob_events the events histogram_event rejected.
+ * Then every worker's queue is released and the plugin can be set up again. */
+int dqdk_gpu_fp_fini(uint32_t* host_hist, int csv_fd, dqdk_gpu_counters_t* totals);
+
 /* ---- raw payload stream (tristan_process write(), src/tristan.c:318-324) -- */
 /* The concatenation, in descriptor order, of payload[0, datalen) of every
  * frame the batch hands to the frame processor (accounted OK frames; in

@@ -45,6 +45,7 @@ def test_struct_layouts_match_header():
     assert C.sizeof(L.Counters) == 12 * 8
     assert C.sizeof(L.Cfg) == 16
     assert C.sizeof(L.SynthCfg) == 24
+    assert C.sizeof(L.FpCfg) == 32
     assert L.HISTO_ENTRIES * 4 == 2_378_170_368  # sizeof(tristan_histo_t), SURVEY §2.1
 
 
@@ -90,3 +91,21 @@ def test_summary_line_matches_tristan_fini_format():
             "\"dqdk_runtime_ms\": %.2lf, \"directory\": \"%s\"}").replace("%llu", "%d").replace("%.2lf", "%.2f") % (
         273, 4374, 3, 2.25, "/data/run1")
     assert s == want
+
+
+def test_frame_processor_plugin_refuses_without_setup_or_device():
+    """dqdk_gpu_frame_processor (the dqdk_frame_processor_t of src/dqdk.h:85)
+    fails like a processor error before dqdk_gpu_fp_init, and the plugin
+    cannot be set up without a gfx950 device (no CPU path behind it)."""
+    import torch
+    lib = L.lib()
+    worker = C.create_string_buffer(64)  # any dqdk_worker address: the plugin keys on the pointer
+    payload = C.create_string_buffer(1458)
+    assert lib.dqdk_gpu_frame_processor(C.addressof(worker), payload, 1458) == -22
+    assert lib.dqdk_gpu_fp_fini(None, -1, None) == -22
+    assert lib.dqdk_gpu_fp_flush(None) == -22
+    assert lib.dqdk_gpu_fp_init(None) == -22
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    cfg = L.FpCfg(L.Cfg(1458, L.MODE_ENERGYHISTO, 0, 0, 0), 0, 0, 0, 0)
+    assert lib.dqdk_gpu_fp_init(C.byref(cfg)) == -19  # ENODEV

@@ -305,3 +305,37 @@ def test_raw_stream_side_stream_multi_batch(tmp_path):
         assert path.read_bytes() == b"".join(want)
     finally:
         os.close(fd)
+
+
+def test_raw_stream_failed_write_finishes_the_batch_first():
+    """A deferred raw write() that fails (here EPIPE: the pipe's reader is
+    gone) is returned by the call that makes it, but only after that call's
+    own batch is complete: its per-frame results and counter delta are the
+    oracle's, and nothing of the batch is still in flight when it returns
+    (the frames are overwritten right after).  ADVICE r3 (high)."""
+    _need_gpu()
+    import errno
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM)
+    r, w = os.pipe()
+    os.close(r)  # EPIPE on write (Python ignores SIGPIPE)
+    q = D.RxQueue(0, cfg, 4096)
+    try:
+        q.set_raw_fd(w)
+        umem, desc = D.synth_umem(4096, 1500, 4096, queue=0, faulty=True)
+        res, _ = q.process_batch(umem, desc)  # batch 0: its write is deferred to the next call
+        q.unregister_umem(umem)
+        umem, desc = D.synth_umem(4096, 1500, 4096, queue=1, faulty=True)
+        ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+        with pytest.raises(D.DqdkError) as e:
+            q.process_batch(umem, desc)  # writes batch 0 -> EPIPE, after batch 1 completed
+        assert e.value.errno == errno.EPIPE
+        umem[:] = 0xCD
+        q.unregister_umem(umem)
+        # batch 1 ran to completion: its counters are in the cumulative ones
+        c = q.counters()
+        assert c["rcvd_pkts"] == 2 * 4096 and c["total_bytes"] > 0
+        with pytest.raises(D.DqdkError):
+            q.set_raw_fd(-1)  # draining batch 1 into the broken pipe fails too
+    finally:
+        q.close()
+        os.close(w)
