@@ -75,6 +75,7 @@ def parse_args(argv=None):
     p.add_argument("--offered-gbps", type=float, default=100.0, help="e2e offered load over all queues (Gbit/s)")
     p.add_argument("--cpu-baseline-sec", type=float, default=8.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-box-state", action="store_true", help="skip the sysfs record of clocks / partitions")
     p.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--share-gpu", action="store_true",
                    help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
@@ -397,6 +398,52 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     }
 
 
+def box_state(torch, dev_index):
+    """The GPU box's memory-system state, recorded in the bench line from this
+    process (the decode runs in one of two per-box speed states):
+    the device's current clock levels (gfx / memory / fabric / SoC), compute
+    and memory partition modes, performance level and temperatures, read from
+    the amdgpu sysfs files of the HIP device's own PCI function (plain
+    read-only file reads; no SMI tool is started), or the error that
+    prevented it."""
+    out = {}
+    try:
+        pr = torch.cuda.get_device_properties(dev_index)
+        bdf = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+        base = Path("/sys/bus/pci/devices") / bdf
+        out["bdf"] = bdf
+
+        def rd(name, n=600):
+            try:
+                return (base / name).read_text()[:n].strip()
+            except OSError as e:
+                return f"<{e.strerror}>"
+
+        def current(text):  # the pp_dpm_* level marked with '*'
+            return next((l.split(":", 1)[1].strip().rstrip("*").strip() for l in text.splitlines()
+                         if l.endswith("*")), text)
+
+        for clk in ("sclk", "mclk", "fclk", "socclk"):
+            t = rd(f"pp_dpm_{clk}")
+            out[f"{clk}_current"] = current(t)
+            out[f"{clk}_levels"] = t.replace("\n", "; ")
+        for f in ("current_compute_partition", "current_memory_partition", "power_dpm_force_performance_level",
+                  "mem_info_vram_total", "mem_info_vram_used"):
+            out[f] = rd(f)
+        temps = {}
+        for hw in sorted((base / "hwmon").glob("hwmon*")):
+            for t in sorted(hw.glob("temp*_input")):
+                lab = t.with_name(t.name.replace("_input", "_label"))
+                try:
+                    temps[lab.read_text().strip() if lab.exists() else t.name] = int(t.read_text()) / 1000
+                except (OSError, ValueError):
+                    pass
+        out["temps_C"] = temps
+    except Exception as e:  # recorded, not fatal: the measurement itself stands
+        out["error"] = f"{type(e).__name__}: {e}"[:400]
+    return out
+
+
 def aggregate_ranks(torch, dist, dev, world, elapsed, t_rank, packets, frame_bytes):
     """Job time = max over ranks of the barrier-bracketed time; per-GPU rates
     from each rank's own time.  Returns (elapsed, per_gpu list or None)."""
@@ -582,6 +629,8 @@ def main():
     for im in images.values():
         torch.cuda.synchronize(dev)
         im.close()
+    if rank == 0 and not args.cpu_dry_run and not args.no_box_state:
+        extra["box_state"] = box_state(torch, dev.index)
     if rank == 0:
         line = {
             "metric": METRIC,

@@ -1,11 +1,11 @@
 """Build the in-tree native libraries (gfx950 HIP + host C).
 
-Outputs (git-ignored; all but oracle/_ref travel to the GPU box with the snapshot):
+Outputs (git-ignored; all travel to the GPU box with the gpurun snapshot):
   dqdk_amd/lib/libdqdk_gpu.so   -- the product: HIP kernels + C ABI (include/dqdk_gpu.h)
   oracle/liboracle.so           -- test-only C restatement (oracle/Makefile)
   build/fetch_xsk_harness       -- test-only C consumer of include/dqdk_gpu.h (tests/c/)
-  oracle/_ref/libref_tcpip.so   -- the reference's src/tcpip, only where /root/reference exists
-                                   (container only: oracle/_ref is listed in .gpurunignore)
+  oracle/_ref/libref_tcpip.so   -- the reference's src/tcpip, built only where /root/reference exists
+                                   (test-only checker, like liboracle.so)
   oracle/_ref/libref_tristan.so -- the reference's TRISTAN decode (oracle/ref_tristan.py), same condition
 """
 from __future__ import annotations

@@ -78,7 +78,8 @@ enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPar
 const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",       "rx_histo_atomic",
                                           "rx_part1",  "(unused)", "rx_part2",       "rx_slice_histo",
                                           "(unused)", "rx_fixup"};
-constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters
+constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters, [20] rx_count's ticket
+constexpr int kTicketWord = 20;
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
 {
@@ -224,6 +225,20 @@ struct dqdk_gpu_queue {
     uint32_t* d_async = nullptr;
     size_t async_cap = 0;  // bursts
     std::vector<Reg> regs;
+    // Host drop-in (dqdk_gpu_rx_batch) without raw egress: the descriptors
+    // are copied into pinned h_desc and read from there by the kernels
+    // (zero-copy), rx_count writes the per-frame results and the batch's
+    // counters straight into pinned h_res / h_batch, and the call returns at
+    // ev_read: after the last kernel that reads caller memory (the frames,
+    // the descriptors); the histogram kernels run on behind it.
+    dqdk_gpu_desc_t* h_desc = nullptr;
+    dqdk_gpu_rx_result_t* h_res = nullptr;
+    uint64_t* h_batch = nullptr;
+    const dqdk_gpu_desc_t* h_desc_dev = nullptr;
+    dqdk_gpu_rx_result_t* h_res_dev = nullptr;
+    uint64_t* h_batch_dev = nullptr;
+    hipEvent_t ev_read = nullptr;
+    bool publish = false;  // this launch: rx_count publishes to h_res / h_batch, ev_read is recorded
     // stage timing
     int timing = 0;
     uint32_t stage_mask = ~0u;  // stages bracketed while timing is on
@@ -368,6 +383,33 @@ uint32_t* records_part1(const dqdk_gpu_queue* q)
     return q->part1_elems >= q->nk_max + kStagePad ? q->d_part1 : q->d_part1_rec;
 }
 
+// Launch guard: when p lies in an allocation of dqdk_gpu_device_alloc
+// (UMEM images, frame staging slots: sizes known exactly), [p, p + bytes)
+// must lie inside it -- the kernels' buffer descriptors and plain pointers
+// reach exactly as far as the caller's sizes say (DESIGN.md section 3 lists
+// each kernel's furthest byte).  Other memory is the caller's to size (HIP's
+// pointer-range attribute is not reliable past 4 GiB on this stack).
+std::mutex g_alloc_mu;
+std::vector<std::pair<uintptr_t, uint64_t>> g_allocs;  // dqdk_gpu_device_alloc: base, size
+
+int check_range(const void* p, uint64_t bytes, const char* what)
+{
+    if (!p || !bytes)
+        return 0;
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    for (const auto& r : g_allocs) {
+        if (a >= r.first && a < r.first + r.second) {
+            if (bytes > r.first + r.second - a) {
+                g_err = std::string(what) + ": runs past the end of its dqdk_gpu_device_alloc allocation";
+                return -EINVAL;
+            }
+            return 0;
+        }
+    }
+    return 0;
+}
+
 // Histogram accumulation of a batch's keys (K3): frame-order records (the
 // atomic path, or rx_part1 -> rx_part2 on the partitioned one), or with fg
 // set the fused decode's pieces + overflow list.  The partitioned path stages
@@ -386,6 +428,8 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     ha.lo = q->d_lo;
     ha.scratch = slot_scratch;
     const bool fused = fg != nullptr;
+    if (partitioned && (q->hist_pending >= q->hist_k || !q->d_part2))
+        return fail_errno(-EIO, "histogram: staging slot out of range");
     ha.part1 = fused ? q->d_part1 : records_part1(q);
     ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
     ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
@@ -418,6 +462,8 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
         StageTimer t(q, fused ? kStFixup : kStPart1);
         hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ra, ha);
     }
+    if (q->publish && fused)  // rx_fixup was the last reader of the caller's frames
+        HIPCHK(hipEventRecord(q->ev_read, q->stream));
     {
         StageTimer t(q, kStPart2);
         // non-temporal key loads where the fused decode's are (fused_policy bit 1)
@@ -511,6 +557,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ca.histo = q->histo;
     ca.batch_scratch = q->d_batch;
     ca.cum = q->d_cum;
+    if (q->publish) {
+        ca.out_res = q->h_res_dev;
+        ca.out_batch = q->h_batch_dev;
+        ca.ticket = (uint32_t*)(q->d_batch + kTicketWord);
+    }
     const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
     {
         StageTimer t(q, kStAbort);
@@ -522,6 +573,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         hipLaunchKernelGGL(rx_count_kernel, dim3(grid_c), dim3(256), 0, q->stream, ca);
     }
     HIPCHK(hipGetLastError());
+    // the records path reads no caller memory past this point (the fused
+    // path's rx_fixup re-reads the frames of checksum-failed ones: its mark
+    // is in launch_histo)
+    if (q->publish && !fused)
+        HIPCHK(hipEventRecord(q->ev_read, q->stream));
 
     if (q->histo && q->E)
         return launch_histo(q, n, d_res, keys, partitioned, fused ? &fg : nullptr, ra, slot_scratch);
@@ -832,7 +888,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             (e = dev_alloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES, q->alloc_kind)) != hipSuccess)
             return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
         if ((e = hipMemset(q->d_hist, 0, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMemset(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess)
+            (e = hipMemset(q->d_lo, 0, DQDK_TRISTAN_HISTO_ENTRIES)) != hipSuccess ||
+            (e = hipStreamSynchronize(nullptr)) != hipSuccess)  // (the fills complete, or fail, here)
             return cleanup(fail("hipMemset(histogram)", e));
         if (q->E) {
             const size_t nk = (size_t)max_batch * q->E;
@@ -927,6 +984,10 @@ int dqdk_gpu_device_alloc(int device, uint64_t size, void** d_out)
     if (e != hipSuccess)
         return (fail("device_alloc", e), -ENOMEM);
     *d_out = p;
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        g_allocs.emplace_back((uintptr_t)p, size);
+    }
     return got == kAllocContig ? 0 : 1;  // 0 only for a physically contiguous range
 }
 
@@ -937,6 +998,14 @@ int dqdk_gpu_device_free(int device, void* d_ptr)
     if (device < 0 || device >= dqdk_gpu_device_count())
         return fail_errno(-ENODEV, "device_free: no such HIP device");
     SETDEV(device);
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        for (size_t k = 0; k < g_allocs.size(); k++)
+            if (g_allocs[k].first == (uintptr_t)d_ptr) {
+                g_allocs.erase(g_allocs.begin() + (long)k);
+                break;
+            }
+    }
     dev_free(d_ptr);
     return 0;
 }
@@ -950,6 +1019,8 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
         (void)raw_drain(q);  // the last batch's raw stream still goes to its file
     if (q->stream)
         (void)hipStreamSynchronize(q->stream);
+    if (q->raw_stream)
+        (void)hipStreamSynchronize(q->raw_stream);  // no D2H into h_rawb may outlive it
     for (auto& r : q->regs)
         (void)hipHostUnregister(r.host);
     for (auto& p : q->pending) {
@@ -983,6 +1054,14 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     }
     if (q->h_raw_total)
         (void)hipHostFree(q->h_raw_total);
+    if (q->h_desc)
+        (void)hipHostFree(q->h_desc);
+    if (q->h_res)
+        (void)hipHostFree(q->h_res);
+    if (q->h_batch)
+        (void)hipHostFree(q->h_batch);
+    if (q->ev_read)
+        (void)hipEventDestroy(q->ev_read);
     if (q->raw_stream)
         (void)hipStreamDestroy(q->raw_stream);
     if (q->switch_ev)
@@ -1029,6 +1108,12 @@ int dqdk_gpu_rx_batch_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_
     if (n == 0)
         return 0;
     SETDEV(q->device);
+    int rc;
+    if ((rc = check_range(d_umem, umem_size, "rx_batch_device: d_umem")) ||
+        (rc = check_range(d_desc, (uint64_t)n * sizeof(dqdk_gpu_desc_t), "rx_batch_device: d_desc")) ||
+        (rc = check_range(d_results, (uint64_t)n * sizeof(dqdk_gpu_rx_result_t), "rx_batch_device: d_results")) ||
+        (rc = check_range(d_keys, (uint64_t)n * q->E * 4u, "rx_batch_device: d_keys")))
+        return rc;
     return launch_batch(q, d_umem, umem_size, d_desc, n, d_results, d_keys);
 }
 
@@ -1104,6 +1189,34 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
         reg = &q->regs.back();
     }
     const uint8_t* dev_umem = (const uint8_t*)reg->dev + (umem - (const uint8_t*)reg->host);
+    if (q->raw_fd < 0) {
+        // the fast form: pinned descriptors / results / counters, return at ev_read
+        if (!q->h_desc) {
+            const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+            hipError_t e;
+            if ((e = hipHostMalloc(&q->h_desc, (size_t)q->max_batch * sizeof(dqdk_gpu_desc_t), fl)) != hipSuccess ||
+                (e = hipHostMalloc(&q->h_res, (size_t)q->max_batch * sizeof(dqdk_gpu_rx_result_t), fl)) != hipSuccess ||
+                (e = hipHostMalloc(&q->h_batch, kBatchScratch * sizeof(uint64_t), fl)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&q->h_desc_dev, q->h_desc, 0)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&q->h_res_dev, q->h_res, 0)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&q->h_batch_dev, q->h_batch, 0)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&q->ev_read, hipEventDisableTiming)) != hipSuccess)
+                return fail("rx_batch: pinned buffers", e);
+        }
+        memcpy(q->h_desc, d, (size_t)n * sizeof(*d));
+        q->publish = true;
+        int rc = launch_batch(q, dev_umem, umem_size, q->h_desc_dev, n, q->d_res, nullptr);
+        q->publish = false;
+        hipError_t e = rc ? hipSuccess : hipEventSynchronize(q->ev_read);
+        if (rc || e != hipSuccess) {  // nothing of the batch may still run once we return
+            const hipError_t e2 = hipStreamSynchronize(q->stream);
+            return rc ? rc : fail("rx_batch: hipEventSynchronize", e != hipSuccess ? e : e2);
+        }
+        memcpy(per_pkt, q->h_res, (size_t)n * sizeof(*per_pkt));
+        if (delta)
+            memcpy(delta, &q->h_batch[1], sizeof(*delta));
+        return 0;
+    }
     HIPCHK(hipMemcpyAsync(q->d_desc, d, (size_t)n * sizeof(*d), hipMemcpyHostToDevice, q->stream));
     // Once the batch is enqueued, no path returns before the queue stream has
     // drained: its kernels read the caller's frames (valid only until this

@@ -79,6 +79,8 @@ __device__ __forceinline__ void load_row(const uint32_t* hist, const uint8_t* lo
     }
 }
 
+// (callers that scan more than once per launch barrier between the scans:
+// lds_wave is rewritten by the next one)
 template <typename T>
 __device__ __forceinline__ T block_excl_scan(T x, T* lds_wave, T* total)
 {
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(1024) void csv_scan_kernel(uint64_t* __restrict__ b
         if (i < nblk)
             blk_chars[i] = carry + ex;
         carry += total;
-        __syncthreads();
+        __syncthreads();  // every wave has read lds before the next chunk's scan rewrites it
     }
     if (threadIdx.x == 0)
         blk_chars[nblk] = carry;

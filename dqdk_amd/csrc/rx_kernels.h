@@ -124,8 +124,13 @@ constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one chu
 // rx_part1 groups afterwards.
 constexpr int kFWaves = 16;
 constexpr int kFThreads = kFWaves * 64;
+// The frame's checksum tail is corrected in the window loop (no 16-KB
+// per-frame tail copy in LDS): that room goes to the bucket stages.
+#ifndef DQDK_INLINE_TAIL
+#define DQDK_INLINE_TAIL 1
+#endif
 #ifndef DQDK_FCAP
-#define DQDK_FCAP 120
+#define DQDK_FCAP (DQDK_INLINE_TAIL ? 134 : 120)
 #endif
 constexpr int kFCap = DQDK_FCAP;
 constexpr uint32_t kTripleMask = (1u << kL1Shift) - 1;  // a bucket-local key
@@ -187,7 +192,14 @@ struct CountArgs {
     int histo;
     uint64_t* batch_scratch;
     dqdk_gpu_counters_t* cum;
+    // host drop-in (dqdk_gpu_rx_batch): the results as read, and the batch's
+    // [first abort idx, counters] once every block has added its counts (the
+    // last block by ticket), written into pinned host memory; null: not kept
+    dqdk_gpu_rx_result_t* out_res;
+    uint64_t* out_batch;  // kBatchOut words
+    uint32_t* ticket;     // zero between launches
 };
+constexpr int kBatchOut = 13;  // batch_scratch[0..12]
 
 struct HistoArgs {
     const dqdk_gpu_rx_result_t* res;

@@ -406,7 +406,7 @@ struct DecodeLds {
 
 // Per-frame stream parameters in the owning lane's VGPRs.
 //   pk1 = nwin | de << 16 | r << 18 | dec << 20 | lw << 21 | th << 22 | tl << 23
-//   pk2 = tw | mw << 16
+//   pk2 = tw | mw << 11 | keep << 22
 // nwin: 2-KiB windows; de: chunk of event 0; r: event shift; dec: decode;
 // lw: some window needs per-lane checksum weights (chunks past ct), the
 // first such window is mw; tw/tl/th: window/lane/half holding the last
@@ -418,7 +418,7 @@ struct LaneFrame {
     int ct;
 };
 
-constexpr uint32_t kNoWin = 0xffffu;
+constexpr uint32_t kNoWin = 0x7ffu;  // (a frame streams at most 513 windows: E <= 65535)
 
 __device__ __forceinline__ uint32_t pk_nwin(uint32_t pk1) { return pk1 & 0xffffu; }
 
@@ -432,6 +432,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const LaneFrame& lf
 struct PFrame {
     uint32_t nwin, de, r, Ef, lw, th, tl, tw, mw;  // Ef = events to decode (0: frame not decoded)
     int ct;
+    uint32_t keep;  // checksum bytes in the last checksum chunk (tail correction when < 16)
 };
 
 __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uint32_t j, PFrame& P)
@@ -444,8 +445,9 @@ __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uin
     P.lw = (pk1 >> 21) & 1u;
     P.th = (pk1 >> 22) & 1u;
     P.tl = pk1 >> 23;
-    P.tw = pk2 & 0xffffu;
-    P.mw = pk2 >> 16;
+    P.tw = pk2 & kNoWin;
+    P.mw = (pk2 >> 11) & kNoWin;
+    P.keep = (pk2 >> 22) & 31u;
     P.ct = P.lw ? (int)rdl((uint32_t)lf.ct, j) : 0;
 }
 
@@ -565,7 +567,7 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
         parse_frame(a, i, fi, r, needB);
     stream = false;
     lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
-    lf.pk2 = kNoWin | (kNoWin << 16);
+    lf.pk2 = kNoWin | (kNoWin << 11);
     lf.ct = -1;
     if (needB) {
         const Geo& g = fi.g;
@@ -587,11 +589,27 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
                  ((fi.work & 1u) << 20) | ((lw ? 1u : 0u) << 21) | (((ct >> 6) & 1u) << 22) | ((ct & 63u) << 23);
         const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
         const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
-        lf.pk2 = tw | (mw << 16);
+        lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22);
         lf.ct = g.ct;
     }
     if (!stream)
         lf.pk1 = 0;
+}
+
+// Word sum of the bytes [keep, 16) of a frame's last checksum chunk: the
+// part of it past the datagram (the odd-length over-read byte is inside
+// keep), which the streamed sum must not contain.
+__device__ __forceinline__ uint32_t tail_corr(const u32x4& tail, int keep)
+{
+    const uint32_t tw4[4] = {tail.x, tail.y, tail.z, tail.w};
+    uint32_t corr = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int lo = keep - 4 * d;  // bytes of dword d inside the datagram
+        const uint32_t m = lo <= 0 ? 0xffffffffu : lo >= 4 ? 0u : (0xffffffffu << (8 * lo));
+        corr = __builtin_amdgcn_udot2(as_u16x2(tw4[d] & m), u16x2{1, 1}, corr, false);
+    }
+    return corr;
 }
 
 // ---- phase C: lane finishes its own frame (checksum verdict, result) ----
@@ -602,16 +620,8 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
         if (fi.work & 2) {
             // tail correction: bytes [keep, 16) of the last checksum chunk lie
             // past the datagram (the odd-length over-read byte is inside keep)
-            uint32_t corr = 0;
-            if (fi.g.ct >= 0 && fi.g.keep < 16) {
-                const uint32_t tw4[4] = {tail.x, tail.y, tail.z, tail.w};
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const int lo = fi.g.keep - 4 * d;  // bytes of dword d inside the datagram
-                    const uint32_t m = lo <= 0 ? 0xffffffffu : lo >= 4 ? 0u : (0xffffffffu << (8 * lo));
-                    corr = __builtin_amdgcn_udot2(as_u16x2(tw4[d] & m), u16x2{1, 1}, corr, false);
-                }
-            }
+            // (the fused decode subtracted it in the window loop: tail is 0 there)
+            const uint32_t corr = fi.g.ct >= 0 && fi.g.keep < 16 ? tail_corr(tail, fi.g.keep) : 0u;
             // udp_csum sums LE words from the UDP start.  tsum summed the words
             // at even addresses: the same words when the UDP header starts at an
             // even address; otherwise every word is byte-swapped, and the one's
@@ -852,7 +862,9 @@ struct FusedLds {
     uint32_t scnt[kL1Buckets + 4];   // staged keys per bucket this round (returning LDS atomics)
     uint32_t sum[kFWaves * 64];      // checksum word sums per frame
     uint32_t oob[kFWaves * 64];      // out-of-bounds events per frame
+#if !DQDK_INLINE_TAIL
     u32x4 tail[kFWaves * 64];        // last checksum chunk per frame
+#endif
     uint32_t wtot[kFWaves];          // windows of each wave's tile
     uint32_t ovf_n;                  // keys in this block's private overflow region
 };
@@ -1186,7 +1198,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (smask0)
             pframe(a, lf, jp, P);
         else
-            P = PFrame{0, 0, 0, 0, 0, 0, 0, kNoWin, kNoWin, 0};
+            P = PFrame{0, 0, 0, 0, 0, 0, 0, kNoWin, kNoWin, 0, 16};
         uint32_t acc0 = 0, acc1 = 0;
         // one loop over the rounds' windows (the flush inside it, every W
         // windows): a single back-edge keeps the compiler's vmcnt accounting
@@ -1205,8 +1217,19 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                     csum_pair(b0[d], b1[d], u16x2{1, 1}, u16x2{1, 1}, acc0, acc1);
                 }
                 if (active && wp == P.tw) {  // (wave-uniform) the frame's last checksum chunk
+#if DQDK_INLINE_TAIL
+                    // its bytes past the datagram leave the sum here, by the
+                    // lane holding it (no per-frame LDS copy for phase C)
+                    if (lane == (int)P.tl) {
+                        if (P.th)
+                            acc1 -= tail_corr(b1[d], (int)P.keep);
+                        else
+                            acc0 -= tail_corr(b0[d], (int)P.keep);
+                    }
+#else
                     if (lane == (int)P.tl)
                         lds.tail[wslot0 + jp] = P.th ? b1[d] : b0[d];
+#endif
                 }
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
@@ -1245,7 +1268,11 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my] / kCntUnit;
         lds.sum[my] = 0;
         lds.oob[my] = 0;
+#if DQDK_INLINE_TAIL
+        phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, u32x4{0u, 0u, 0u, 0u});
+#else
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
+#endif
         // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
         if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
             a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
@@ -1426,8 +1453,11 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
             r[u] = i0 + u * stride < a.n ? *(const uint2*)&a.res[i0 + u * stride] : make_uint2(0u, 0xffu);
 #pragma unroll
         for (int u = 0; u < kU; u++)
-            if (i0 + u * stride < a.n)
+            if (i0 + u * stride < a.n) {
                 count(i0 + u * stride, __builtin_bit_cast(dqdk_gpu_rx_result_t, r[u]));
+                if (a.out_res)  // the host drop-in's per_pkt, straight into pinned host memory
+                    ((uint2*)a.out_res)[i0 + u * stride] = r[u];
+            }
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -1462,6 +1492,25 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
         b[11] = abort_idx;               // first_abort_idx of this batch
         cum[11] = abort_idx;
     }
+    if (a.out_batch) {
+        // the last block to finish publishes the batch's counters to the host
+        __shared__ uint32_t last;
+        __threadfence();  // this block's counter adds (and block 0's stores) before its ticket
+        __syncthreads();
+        if (threadIdx.x == 0)
+            last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (last) {
+            __threadfence();
+            if (threadIdx.x < kBatchOut)
+                a.out_batch[threadIdx.x] =
+                    __hip_atomic_load(&a.batch_scratch[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0)
+                *a.ticket = 0;
+        }
+    }
+    if (a.out_res || a.out_batch)
+        __threadfence_system();  // host-memory writes visible once the kernel completes
 }
 
 // ---------------------------------------------------------------------------

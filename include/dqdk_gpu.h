@@ -131,7 +131,23 @@ typedef struct dqdk_gpu_queue dqdk_gpu_queue_t;
 int dqdk_gpu_abi_version(void);
 int dqdk_gpu_device_count(void);
 /* One queue per RX queue / worker thread (src/dqdk.c:517-620).  Allocates
- * the queue's device histogram (2.38 GB, zeroed) unless the mode has none. */
+ * the queue's device histogram (2.38 GB, zeroed) unless the mode has none.
+ *
+ * HBM per queue with a histogram (max_batch = 1M frames, E = payloadsz/16):
+ *                                         1M x 1500 B (E 91)   1M x 9000 B (E 559)
+ *   table: u32 base + u8 low plane          2.97 GB              2.97 GB
+ *   fused pieces (key triples, 1.25x)       0.34 GB              1.97 GB
+ *   overflow regions + list (2 x 256 x      0.13 GB              0.59 GB
+ *     max(64K, 1/8 of a block's keys))
+ *   slice staging, per staged batch         0.22 GB              1.20 GB
+ *     x batches per pass                    x 32 = 7.0 GB        x 21 = 25.2 GB
+ *   descriptors, results, scratch           0.03 GB              0.03 GB
+ *   total                                   ~10.5 GB             ~30.8 GB
+ * The staging takes at most 24 GiB or a quarter of the device memory free at
+ * creation, and halves while its allocation fails (down to one batch per
+ * pass).  The records path (frame-order keys: BATCH_ABORT, HISTO_UNFUSED, or
+ * batches too small to partition) adds n * E * 8 B (keys + their grouped copy)
+ * on its first batch -- allocated at creation when the flags force it. */
 int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_batch, dqdk_gpu_queue_t** out);
 int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q);
 /* Queues start on a stream of their own (hipStreamNonBlocking).  Run the
@@ -292,8 +308,8 @@ int dqdk_gpu_histogram_reset(dqdk_gpu_queue_t* q);
 uint32_t* dqdk_gpu_histogram_device_ptr(dqdk_gpu_queue_t* q);
 /* Partitioned batches stage their slice-sorted events and the slice pass
  * (the sweep of the table's low-byte plane) runs once per
- * batches_per_pass staged batches (up to 32, as many as a 24 GB staging
- * budget holds: 32 at 1M x 1500 B, 20 at 1M x 9000 B; DQDK_GPU_F_HISTO_EAGER:
+ * batches_per_pass staged batches (up to 32, as many as the staging budget
+ * above holds: 32 at 1M x 1500 B, 21 at 1M x 9000 B; DQDK_GPU_F_HISTO_EAGER:
  * 1).  Every histogram reader above and below flushes first; flush runs
  * the pending slice pass now (async on the queue stream). */
 int dqdk_gpu_histogram_flush(dqdk_gpu_queue_t* q);

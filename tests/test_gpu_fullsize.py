@@ -120,6 +120,23 @@ def test_fused_peaked_faulty_overflows_pieces():
     assert int(otable.max()) > 0xFFFF
 
 
+@pytest.mark.parametrize("L,stride,payloadsz", [(1500, 4096, 1458), (9000, 9216, 8958)])
+def test_fused_overflow_regions_spill_to_the_table(monkeypatch, L, stride, payloadsz):
+    """The fused decode's per-block overflow regions are bounded (64K keys, or
+    an eighth of a block's keys); past that a key goes to the table by a
+    device atomic.  With the regions forced down to 64 keys (DQDK_GPU_OVF_BLK)
+    and the peaked spectrum overflowing every round, most overflow keys take
+    that spill: the table, results and counters still equal the oracle's."""
+    monkeypatch.setenv("DQDK_GPU_OVF_BLK", "64")
+    n = 1 << 18
+    umem, desc = D.synth_umem(n, L, stride, faulty=True, peaked=True, threads=HOST_THREADS)
+    cfg = D.RxConfig(payloadsz=payloadsz, flags=D.F_CSUM)
+    res, cnt, table, launches = run_bench_form(umem, desc, cfg)
+    assert launches.get("rx_fixup", 0) == 1, launches
+    ores, ocnt, otable = oracle_full(umem, desc, cfg)
+    assert_same(res, cnt, table, ores, ocnt, otable)
+
+
 def test_records_path_full_size_vs_oracle():
     """The records path (frame-order 4-B records, rx_part1 grouping them) at
     1M x 1500 B: every result, record, counter and the whole table."""

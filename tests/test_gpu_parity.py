@@ -468,3 +468,23 @@ def test_staged_slice_pass_flush_and_reset():
     nz = np.flatnonzero(hist)
     np.testing.assert_array_equal(nz, u)
     np.testing.assert_array_equal(hist[nz], c)
+
+
+def test_launch_guard_refuses_umem_past_its_allocation():
+    """Host-side launch guard: a UMEM image from dqdk_gpu_device_alloc whose
+    stated umem_size runs past the allocation is refused with -EINVAL before
+    any kernel reads past it (the kernels' buffer extents come from the
+    caller's sizes)."""
+    _need_gpu()
+    umem, desc = D.synth_umem(256, 1500, 4096)
+    with D.DeviceBuffer(0, umem.nbytes) as img, D.RxQueue(0, D.RxConfig(payloadsz=1458), 256) as q:
+        img.tensor.copy_(torch.from_numpy(umem))
+        d_desc = torch.from_numpy(desc.view(np.uint8)).cuda()
+        d_res = torch.zeros(256 * 8, dtype=torch.uint8, device="cuda:0")
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        with pytest.raises(D.DqdkError) as e:
+            q.process_device(img.ptr, umem.nbytes + 4096, d_desc.data_ptr(), 256, d_res.data_ptr())
+        assert e.value.errno == 22
+        q.process_device(img.ptr, umem.nbytes, d_desc.data_ptr(), 256, d_res.data_ptr())  # exact: fine
+        torch.cuda.synchronize()
+        assert q.counters()["rcvd_pkts"] == 256
