@@ -478,6 +478,8 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     return 0;
 }
 
+bool small_off();
+
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
 {
@@ -513,6 +515,20 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (partitioned)
         HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
 
+    CountArgs ca{};
+    ca.res = d_res;
+    ca.n = n;
+    ca.E = q->E;
+    ca.flags = q->cfg.flags;
+    ca.histo = q->histo;
+    ca.batch_scratch = q->d_batch;
+    ca.cum = q->d_cum;
+    if (q->publish) {
+        ca.out_res = q->h_res_dev;
+        ca.out_batch = q->h_batch_dev;
+    }
+    ca.ticket = (uint32_t*)(q->d_batch + kTicketWord);
+
     if (fused) {
         ra.keys = nullptr;  // no frame-order records
         ra.scratch = slot_scratch;
@@ -538,6 +554,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
                   : pol == 2 ? rx_decode_fused_kernel<2, false>
                              : rx_decode_fused_kernel<2, true>;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+    } else if (n <= (uint32_t)kTile && !small_off()) {
+        // one block: decode, abort and count in a single launch (rx_small)
+        StageTimer t(q, kStDecode);
+        hipLaunchKernelGGL(rx_small_kernel, dim3(1), dim3(kTile), 0, q->stream, ra, ca);
     } else {
         const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
@@ -549,30 +569,19 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     HIPCHK(hipGetLastError());
 
-    CountArgs ca{};
-    ca.res = d_res;
-    ca.n = n;
-    ca.E = q->E;
-    ca.flags = q->cfg.flags;
-    ca.histo = q->histo;
-    ca.batch_scratch = q->d_batch;
-    ca.cum = q->d_cum;
-    if (q->publish) {
-        ca.out_res = q->h_res_dev;
-        ca.out_batch = q->h_batch_dev;
-        ca.ticket = (uint32_t*)(q->d_batch + kTicketWord);
+    if (fused || n > (uint32_t)kTile || small_off()) {
+        const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
+        {
+            StageTimer t(q, kStAbort);
+            hipLaunchKernelGGL(rx_abort_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
+        }
+        {
+            StageTimer t(q, kStCount);
+            const uint32_t grid_c = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count);
+            hipLaunchKernelGGL(rx_count_kernel, dim3(grid_c), dim3(256), 0, q->stream, ca);
+        }
+        HIPCHK(hipGetLastError());
     }
-    const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
-    {
-        StageTimer t(q, kStAbort);
-        hipLaunchKernelGGL(rx_abort_kernel, dim3(grid_cnt), dim3(256), 0, q->stream, ca);
-    }
-    {
-        StageTimer t(q, kStCount);
-        const uint32_t grid_c = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count);
-        hipLaunchKernelGGL(rx_count_kernel, dim3(grid_c), dim3(256), 0, q->stream, ca);
-    }
-    HIPCHK(hipGetLastError());
     // the records path reads no caller memory past this point (the fused
     // path's rx_fixup re-reads the frames of checksum-failed ones: its mark
     // is in launch_histo)
@@ -582,6 +591,16 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (q->histo && q->E)
         return launch_histo(q, n, d_res, keys, partitioned, fused ? &fg : nullptr, ra, slot_scratch);
     return 0;
+}
+
+// DQDK_GPU_SMALL=0: small batches take the three-launch form too (A/B only)
+bool small_off()
+{
+    static const bool off = [] {
+        const char* v = getenv("DQDK_GPU_SMALL");
+        return v && !strcmp(v, "0");
+    }();
+    return off;
 }
 
 // The frame-processor plugin's batch (frame_processor.hip): n staged

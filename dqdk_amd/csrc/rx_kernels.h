@@ -251,6 +251,7 @@ __global__ void fp_decode_kernel(PayloadArgs a);
 template <int kLdAux, bool kLines>
 __global__ void rx_decode_fused_kernel(RxArgs a);
 __global__ void rx_abort_kernel(CountArgs a);
+__global__ void rx_small_kernel(RxArgs ra, CountArgs ca);  // gridDim 1, n <= kTile, records path
 __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);
 __global__ void rx_part1_kernel(RxArgs ra, HistoArgs a);

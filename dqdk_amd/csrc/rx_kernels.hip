@@ -758,9 +758,8 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     }
 }
 
-__global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
+__device__ __forceinline__ void decode_block(const RxArgs& a, DecodeLds& lds)
 {
-    __shared__ DecodeLds lds;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = rfl((uint32_t)(tid >> 6));
@@ -781,6 +780,12 @@ __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
             if (lds.cnt[b])
                 atomicAdd(&a.cnt1[b], lds.cnt[b]);
     }
+}
+
+__global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
+{
+    __shared__ DecodeLds lds;
+    decode_block(a, lds);
 }
 
 // ===========================================================================
@@ -1385,7 +1390,7 @@ __device__ __forceinline__ bool in_batch(uint32_t st)
 
 constexpr int kAbortLoads = 8;  // result loads in flight per thread (independent: no break between them)
 
-__global__ void __launch_bounds__(256) rx_abort_kernel(CountArgs a)
+__device__ __forceinline__ void abort_block(const CountArgs& a)
 {
     uint64_t m = a.n;
     const uint32_t stride = gridDim.x * 256;
@@ -1410,12 +1415,14 @@ __global__ void __launch_bounds__(256) rx_abort_kernel(CountArgs a)
         atomicMin((unsigned long long*)&a.batch_scratch[0], (unsigned long long)m);
 }
 
+__global__ void __launch_bounds__(256) rx_abort_kernel(CountArgs a) { abort_block(a); }
+
 enum { C_FRAMES, C_PKTS, C_BYTES, C_IP, C_UDP, C_EVENTS, C_TBYTES, C_OOB, C_EMPTY, C_FILT, C_N };
 
-__global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
+__device__ __forceinline__ void count_block(const CountArgs& a)
 {
     __shared__ uint64_t red[C_N][4];
-    const uint64_t abort_idx = a.batch_scratch[0];
+    const uint64_t abort_idx = __hip_atomic_load(&a.batch_scratch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t limit = (a.flags & DQDK_GPU_F_BATCH_ABORT) ? (abort_idx < a.n ? abort_idx + 1 : a.n) : a.n;
     uint64_t c[C_N];
 #pragma unroll
@@ -1511,6 +1518,24 @@ __global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a)
     }
     if (a.out_res || a.out_batch)
         __threadfence_system();  // host-memory writes visible once the kernel completes
+}
+
+__global__ void __launch_bounds__(256) rx_count_kernel(CountArgs a) { count_block(a); }
+
+// A batch of at most kTile frames in one launch: the decode (records path),
+// then this block's own rx_abort and rx_count over the results it just
+// wrote -- one launch instead of three for DQDK's small RX batches (-b 64,
+// src/tristan.c:393), where the launches are the call's latency.
+__global__ void __launch_bounds__(kTile) rx_small_kernel(RxArgs ra, CountArgs ca)
+{
+    __shared__ DecodeLds lds;
+    decode_block(ra, lds);
+    __threadfence();  // the results and the batch-state reset, before the block reads them back
+    __syncthreads();
+    abort_block(ca);
+    __threadfence();
+    __syncthreads();
+    count_block(ca);
 }
 
 // ---------------------------------------------------------------------------

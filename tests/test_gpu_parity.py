@@ -488,3 +488,28 @@ def test_launch_guard_refuses_umem_past_its_allocation():
         q.process_device(img.ptr, umem.nbytes, d_desc.data_ptr(), 256, d_res.data_ptr())  # exact: fine
         torch.cuda.synchronize()
         assert q.counters()["rcvd_pkts"] == 256
+
+
+@pytest.mark.parametrize("flags", [D.F_CSUM, D.F_CSUM | D.F_BATCH_ABORT, D.F_PREFILTER])
+@pytest.mark.parametrize("n", [1, 64, 255, 256])
+def test_small_batches_single_launch(n, flags):
+    """Batches of at most 256 frames (DQDK's default -b 64, src/tristan.c:393)
+    run decode, abort and count in one launch (rx_small): results, records,
+    counters and table equal the oracle's, for the device form and for the
+    host drop-in (pinned descriptors / results, return at the last read of
+    the caller's frames), under both accountings."""
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, first=7 * n)
+    cfg = D.RxConfig(payloadsz=1458, flags=flags | D.F_HISTO_ATOMIC, port_start=5000, port_end=5000)
+    compare(umem, desc, cfg, check_hist=True)
+    with D.RxQueue(0, cfg, 256) as q:
+        q.enable_timing(True)
+        res, delta = q.process_batch(umem, desc)
+        t = q.read_timing()
+        assert t["rx_decode"]["launches"] == 1 and t["rx_abort"]["launches"] == 0  # one launch for the three
+        ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags, cfg.port_start,
+                                   cfg.port_end)
+        np.testing.assert_array_equal(res, ores)
+        for k in ("rcvd_pkts", "rcvd_bytes", "invalid_ip_pkts", "invalid_udp_pkts", "total_events", "total_bytes",
+                  "oob_events", "first_abort_idx", "failing_batches"):
+            assert delta[k] == ocnt[k], (k, delta[k], ocnt[k])
+        q.unregister_umem(umem)
