@@ -330,9 +330,9 @@ int hist_flush(dqdk_gpu_queue* q)
 }
 
 // Windows per wave per fused round: the block's 16 waves stage at most
-// 16 * W * min(E, 128) keys per round into 284 * kFCap slots (kFCap 120).
-// Measured (A/B, one box each): W = 16 at 1500 B (~68 % mean fill; 12 and 20
-// windows lost 1 % and 5 %), W = 12 at 9000 B, where the lines policy
+// 16 * W * min(E, 128) keys per round into 284 * kFCap slots (kFCap 134).
+// Measured (A/B, one box each): W = 16 at 1500 B (~61 % mean fill; 12 and 20
+// windows lost 1 % and 5-7 %), W = 12 at 9000 B, where the lines policy
 // carries up to 47 keys per bucket between rounds (16 windows overflowed
 // three times as many keys to rx_part1; 8 cost the decode more).
 //
@@ -350,8 +350,8 @@ uint32_t fused_policy(uint32_t E) { return DQDK_FUSED_POLICY; }
 uint32_t fused_round_windows(uint32_t E)
 {
     const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
-#ifndef DQDK_FUSED_FILL
-#define DQDK_FUSED_FILL (E >= 128 ? 80 : 75)
+#ifndef DQDK_FUSED_FILL  // (134-key stage: W = 16 at 1500 B, 12 at 9000 B; A/B r04g: 20 / 16 slower)
+#define DQDK_FUSED_FILL (E >= 128 ? 65 : 61)
 #endif
     const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth
@@ -555,7 +555,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
                              : rx_decode_fused_kernel<2, true>;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
     } else if (n <= (uint32_t)kTile && !small_off()) {
-        // one block: decode, abort and count in a single launch (rx_small)
+        // one block: decode, abort and count in a single launch (rx_small),
+        // the frames spread over all its waves (a 64-frame batch is four
+        // 16-frame tiles, not one wave streaming 64 frames in a row: over
+        // zero-copy host UMEM every window is a PCIe round trip)
+        ra.tile_frames = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + kWaves - 1) / kWaves));
         StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_small_kernel, dim3(1), dim3(kTile), 0, q->stream, ra, ca);
     } else {

@@ -182,6 +182,8 @@ struct RxArgs {
     uint32_t* hist;           //   the table's base plane by a device atomic (exact: value = base + low)
     uint32_t* fix;            // decoded frames whose final status is not OK (n)
     uint32_t round_windows;   // windows per wave per round (multiple of the ring depth)
+    uint32_t tile_frames;     // records path: frames per wave tile (0 = 64; fewer spread a small
+                              //   batch over more waves, the host drop-in's zero-copy frames)
 };
 
 struct CountArgs {

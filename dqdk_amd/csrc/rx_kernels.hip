@@ -656,11 +656,11 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
     }
 }
 
-__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, int lane, uint32_t wave,
-                                                 DecodeLds& lds)
+__device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, uint32_t F, int lane,
+                                                 uint32_t wave, DecodeLds& lds)
 {
-    const uint32_t i = tile * 64 + lane;
-    const bool live = i < a.n;
+    const uint32_t i = tile * F + lane;
+    const bool live = (uint32_t)lane < F && i < a.n;
     const uint32_t wslot0 = wave * 64;
 
     // ---- phase A: lane parses frame i ----
@@ -675,7 +675,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     if (smask0) {
         const int total = (int)wave_sum_dpp(pk_nwin(lf.pk1));
         const __amdgpu_buffer_rsrc_t keys_rsrc =
-            uniform_rsrc(a.keys + (uint64_t)tile * 64 * a.E, a.keys ? (uint64_t)64 * a.E * 4u : 0u);
+            uniform_rsrc(a.keys + (uint64_t)tile * F * a.E, a.keys ? (uint64_t)F * a.E * 4u : 0u);
         const uint32_t lane16 = (uint32_t)lane * 16u;
         // load cursor
         uint64_t lmask = smask0;
@@ -770,9 +770,10 @@ __device__ __forceinline__ void decode_block(const RxArgs& a, DecodeLds& lds)
     if (blockIdx.x == 0 && tid < 17)
         a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
 
-    const uint32_t ntiles = (a.n + 63) / 64;
+    const uint32_t F = a.tile_frames ? a.tile_frames : 64u;
+    const uint32_t ntiles = (a.n + F - 1) / F;
     for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves)
-        decode_wave_tile(a, t, lane, wave, lds);
+        decode_wave_tile(a, t, F, lane, wave, lds);
 
     if (a.cnt1) {
         __syncthreads();

@@ -16,8 +16,12 @@ from __future__ import annotations
 import argparse
 import ctypes as C
 import json
+import sys
+from pathlib import Path
 
 import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 from dqdk_amd import _lib as L
 
