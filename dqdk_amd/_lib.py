@@ -104,6 +104,7 @@ SIGNATURES = {
     "dqdk_gpu_raw_compact_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P, _P, C.c_uint64,
                                               C.POINTER(C.c_uint64)]),
     "dqdk_gpu_queue_set_raw_fd": (C.c_int, [_P, C.c_int]),
+    "dqdk_gpu_queue_set_raw_deferred": (C.c_int, [_P, C.c_int]),
     "dqdk_gpu_async_process_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, C.c_uint64,
                                                 C.POINTER(C.c_uint64)]),
     "dqdk_gpu_histogram_copy": (C.c_int, [_P, _P]),

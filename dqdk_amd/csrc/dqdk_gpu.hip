@@ -220,7 +220,7 @@ struct dqdk_gpu_queue {
     int raw_pend[2] = {0, 0};
     uint64_t raw_seq = 0;
     uint64_t* h_raw_total = nullptr;  // pinned: the batch's stream length
-    int raw_sync = 0;                 // DQDK_GPU_RAW_SYNC=1: serial gather -> copy -> write() (A/B only)
+    int raw_deferred = 0;             // dqdk_gpu_queue_set_raw_deferred: write() during the next call
     // async consumer: per-burst first element / length / output offset
     uint32_t* d_async = nullptr;
     size_t async_cap = 0;  // bursts
@@ -341,11 +341,19 @@ int hist_flush(dqdk_gpu_queue* q)
 // 128 on (9000 B: every 2-KB window full of events) whole lines are flushed
 // and remainders carried, which costs stage room, hence the smaller round
 // (A/B, one box, 9000 B: decode 2.86 -> 2.44 ms; at 1500 B lines cost 0.04 ms).
-// policy bit 0: whole-line flushes, bit 1: non-temporal frame loads
+// policy bit 0: whole-line flushes, bit 1: non-temporal frame loads, bit 2:
+// phase A takes each frame's first line (events and checksum bytes; its room
+// in the stage is the round sizing's margin, so only with triples flushes,
+// whose carry is at most 2 keys per bucket).  DQDK_GPU_FUSED_POLICY=<0..7>
+// overrides it per batch (A/B on one box; the tests run every variant).
 #ifndef DQDK_FUSED_POLICY
-#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 2u)
+#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 6u)
 #endif
-uint32_t fused_policy(uint32_t E) { return DQDK_FUSED_POLICY; }
+uint32_t fused_policy(uint32_t E)
+{
+    const char* s = getenv("DQDK_GPU_FUSED_POLICY");
+    return s && *s ? (uint32_t)atoi(s) & 7u : (uint32_t)(DQDK_FUSED_POLICY);
+}
 
 uint32_t fused_round_windows(uint32_t E)
 {
@@ -549,10 +557,12 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         StageTimer t(q, kStDecode);
         // partial-line policy by frame density (fused_policy)
         const uint32_t pol = fused_policy(q->E);
-        auto kern = pol == 0 ? rx_decode_fused_kernel<0, false>
-                  : pol == 1 ? rx_decode_fused_kernel<0, true>
-                  : pol == 2 ? rx_decode_fused_kernel<2, false>
-                             : rx_decode_fused_kernel<2, true>;
+        static void (*const kFused[8])(RxArgs) = {
+            rx_decode_fused_kernel<0, false, false>, rx_decode_fused_kernel<0, true, false>,
+            rx_decode_fused_kernel<2, false, false>, rx_decode_fused_kernel<2, true, false>,
+            rx_decode_fused_kernel<0, false, true>,  rx_decode_fused_kernel<0, true, true>,
+            rx_decode_fused_kernel<2, false, true>,  rx_decode_fused_kernel<2, true, true>};
+        auto kern = kFused[pol & 7u];
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
     } else if (n <= (uint32_t)kTile && !small_off()) {
         // one block: decode, abort and count in a single launch (rx_small),
@@ -788,10 +798,13 @@ int raw_drain(dqdk_gpu_queue* q)
     return rc;
 }
 
-// Serial form (DQDK_GPU_RAW_SYNC=1, kept for the A/B): size query, gather,
-// D2H and write() of the batch, all before returning.
-int write_raw_sync(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint32_t n)
+// Synchronous form (the default, as tristan_process's write, src/tristan.c:
+// 318-324): size query, gather, D2H and write() of the batch, all before the
+// call returns.  Device / runtime failures are returned; the write()'s own
+// result goes to *werr.
+int write_raw_sync(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, uint32_t n, int* werr)
 {
+    *werr = 0;
     int rc = launch_raw(q, d_umem, umem_size, q->d_desc, n, q->d_res, nullptr, 0, false);
     uint64_t total = 0;
     if (!rc)
@@ -805,7 +818,8 @@ int write_raw_sync(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size,
         return rc;
     HIPCHK(hipMemcpyAsync(q->h_rawb[0], q->d_rawb[0], total, hipMemcpyDeviceToHost, q->stream));
     HIPCHK(hipStreamSynchronize(q->stream));
-    return write_fd(q->raw_fd, q->h_rawb[0], total);
+    *werr = write_fd(q->raw_fd, q->h_rawb[0], total);
+    return 0;
 }
 
 }  // namespace
@@ -882,8 +896,6 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     if (const char* v = getenv("DQDK_GPU_DECODE_CUS"))
         q->dec_cus = std::max(1, std::min(q->cu_count, atoi(v)));
     q->alloc_kind = internal_alloc_kind(q->E);
-    if (const char* rs = getenv("DQDK_GPU_RAW_SYNC"))
-        q->raw_sync = atoi(rs) != 0;
     if (cfg->flags & DQDK_GPU_F_HISTO_ATOMIC)
         q->histo_path = 1;
     else if (cfg->flags & DQDK_GPU_F_HISTO_PARTITIONED)
@@ -1038,8 +1050,10 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     if (!q)
         return -EINVAL;
     DevGuard dev_guard_(q->device);
-    if (q->raw_fd >= 0)
-        (void)raw_drain(q);  // the last batch's raw stream still goes to its file
+    int rc = 0;
+    if (q->raw_fd >= 0 && (rc = raw_drain(q)) != 0)  // the last batch's raw stream still goes to its file
+        fprintf(stderr, "dqdk_gpu_queue_destroy: the last deferred raw batch was not written to fd %d: %s\n",
+                q->raw_fd, strerror(-rc));
     if (q->stream)
         (void)hipStreamSynchronize(q->stream);
     if (q->raw_stream)
@@ -1252,7 +1266,8 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
     int rc = launch_batch(q, dev_umem, umem_size, q->d_desc, n, q->d_res, nullptr);
     if (rc)
         return drained(rc);
-    const bool raw = q->raw_fd >= 0 && !q->raw_sync;
+    const bool raw = q->raw_fd >= 0 && q->raw_deferred;
+    int swerr = 0;  // the synchronous form's write() result, returned once the batch is delivered
     const int k = (int)(q->raw_seq & 1);
     uint64_t cap = 0;
     hipError_t e = hipSuccess;
@@ -1280,7 +1295,7 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
         if ((e = hipMemcpyAsync(q->h_raw_total, q->d_raw_blk + nblk, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                 q->stream)) != hipSuccess)
             return drained(fail("hipMemcpyAsync", e));
-    } else if (q->raw_fd >= 0 && (rc = write_raw_sync(q, dev_umem, umem_size, n)) != 0) {
+    } else if (q->raw_fd >= 0 && (rc = write_raw_sync(q, dev_umem, umem_size, n, &swerr)) != 0) {
         return drained(rc);
     }
     uint64_t b[kBatchScratch];
@@ -1321,7 +1336,7 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
         if (total > cap && (rc = drained(0)) != 0)  // the second gather read the frames: done before returning
             return rc;
     }
-    return werr;
+    return werr ? werr : swerr;
 }
 
 int dqdk_gpu_counters_get(dqdk_gpu_queue_t* q, dqdk_gpu_counters_t* out)
@@ -1532,6 +1547,19 @@ int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd)
             return rc;
     }
     q->raw_fd = fd;
+    return 0;
+}
+
+int dqdk_gpu_queue_set_raw_deferred(dqdk_gpu_queue_t* q, int on)
+{
+    if (!q)
+        return -EINVAL;
+    if (q->raw_deferred && !on && q->raw_fd >= 0) {  // what is pending is written first
+        SETDEV(q->device);
+        if (int rc = raw_drain(q))
+            return rc;
+    }
+    q->raw_deferred = on != 0;
     return 0;
 }
 

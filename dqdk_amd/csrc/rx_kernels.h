@@ -250,7 +250,7 @@ struct PayloadArgs {
 
 __global__ void rx_decode_kernel(RxArgs a);
 __global__ void fp_decode_kernel(PayloadArgs a);
-template <int kLdAux, bool kLines>
+template <int kLdAux, bool kLines, bool kHeadA>
 __global__ void rx_decode_fused_kernel(RxArgs a);
 __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_small_kernel(RxArgs ra, CountArgs ca);  // gridDim 1, n <= kTile, records path

@@ -29,18 +29,25 @@ struct Geo {
     int c_begin;     // first streamed chunk
     int nch;         // streamed chunks
     int nwin;        // 2-KiB windows (128 chunks)
-    int de;          // chunk of event 0, relative to c_begin
-    int ct;          // last checksum chunk relative to c_begin (-1: no checksum bytes)
+    int de;          // chunk of event 0, relative to c_begin (-7..1: negative when phase A took events)
+    int ct;          // last checksum chunk relative to c_begin (-1: no checksum bytes streamed)
     int keep;        // checksum bytes in chunk ct (1..16)
     int cs_lo;       // checksum start (a0-relative): bytes [16 c_begin + q4, cs_lo) are the head correction
+    int cs_hi;       // checksum end (a0-relative, the odd-length over-read byte included)
 };
 
 constexpr int kLaneBytes = 32;                    // two chunks per lane per window
 constexpr int kWinChunks = 64 * kLaneBytes / 16;  // 128
 constexpr uint32_t kWinBytes = 64u * kLaneBytes;  // 2 KiB
 
+//
+// a_end > 0 (the fused decode at 1500 B): phase A, which read the frame's
+// first cache line [0, a_end) already, decodes every event whose chunk ends
+// inside it and sums the checksum bytes before the chunk holding byte a_end;
+// the stream starts at that chunk, so phase B re-reads no more of that line
+// than its last chunk's head.
 __device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t poff, uint32_t hs, uint32_t len16,
-                                         uint32_t E)
+                                         uint32_t E, int a_end = 0)
 {
     Geo g;
     const bool dec = work & 1, cs = work & 2;
@@ -52,6 +59,7 @@ __device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t 
     g.q4 = q & 15;
     g.r = (dec_lo + 2) & 3;
     g.cs_lo = cs_lo;
+    g.cs_hi = cs_hi;
     int lo = 0x7fffffff, hi = 0;
     if (dec) {
         lo = dec_lo;
@@ -67,11 +75,15 @@ __device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t 
         return g;
     }
     g.c_begin = (lo - g.q4) >> 4;  // lo >= 14 > q4
-    g.nch = ((hi - g.q4 + 15) >> 4) - g.c_begin;
+    if (a_end > 0)
+        g.c_begin = max(g.c_begin, (a_end - g.q4) >> 4);  // (a_end >= 16 > q4)
+    g.nch = max(((hi - g.q4 + 15) >> 4) - g.c_begin, 0);
     g.nwin = (g.nch + kWinChunks - 1) / kWinChunks;
-    g.de = dec ? (q >> 4) - g.c_begin : 0;  // 0 or 1 (the chunk of event byte 2 is c_begin or the next)
-    if (cs && cs_hi > cs_lo) {
-        const int ct = (cs_hi - 1 - g.q4) >> 4;
+    // 0 or 1 (the chunk of event byte 2 is c_begin or the next); negative:
+    // phase A decoded -de events
+    g.de = dec ? (q >> 4) - g.c_begin : 0;
+    const int ct = (cs_hi - 1 - g.q4) >> 4;
+    if (cs && cs_hi > cs_lo && ct >= g.c_begin) {
         g.ct = ct - g.c_begin;
         g.keep = cs_hi - (16 * ct + g.q4);
     } else {
@@ -125,22 +137,45 @@ __device__ __forceinline__ void chunk_range_sums(uint32_t x0, uint32_t x1, uint3
 }
 
 
+// Events phase A decodes from the frame's first line (kHeadA): at most 7
+// (event 0's chunk starts at or after a0-relative byte 24, the line ends by 128).
+constexpr int kAEv = 7;
+
+// Word sum (LE u16 at even a0-relative addresses) of the bytes [lo, hi) of
+// the 128 B staged from a0.
+__device__ __forceinline__ uint32_t staged_range_sum(const uint32_t (&w)[32], int lo, int hi)
+{
+    auto below = [](int n) -> uint32_t { return n <= 0 ? 0u : n >= 4 ? 0xffffffffu : ((1u << (8 * n)) - 1u); };
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        const uint32_t m = below(hi - 4 * k) & ~below(lo - 4 * k);
+        s = __builtin_amdgcn_udot2(as_u16x2(w[k] & m), u16x2{1, 1}, s, false);
+    }
+    return s;
+}
+
 // ---------------------------------------------------------------------------
-// Phase A: one lane parses one frame's headers from 112 B staged in VGPRs.
+// Phase A: one lane parses one frame's headers from 128 B staged in VGPRs.
+// kHeadA: it also decodes the events and sums the checksum bytes of the
+// frame's first cache line (frame_geo's a_end) into akey[0, na) / fi.head.
 // ---------------------------------------------------------------------------
+template <bool kHeadA>
 __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameInfo& fi, dqdk_gpu_rx_result_t& r,
-                                            bool& needB)
+                                            bool& needB, uint32_t (&akey)[kAEv], uint32_t& na)
 {
     dqdk_gpu_desc_t d = a.desc[i];
     const uint64_t addr = d.addr;
     const uint32_t len = d.len;
     const uint64_t a0 = addr & ~15ull;
     const uint32_t off0 = (uint32_t)(addr & 15);
+    na = 0;
 
-    // 7 aligned chunks = 112 B from a0: covers frame bytes [0, 97) for any off0.
-    uint32_t w[28];
+    // 8 aligned chunks = 128 B from a0: covers frame bytes [0, 113) for any off0
+    // (the headers need [0, 97)).
+    uint32_t w[32];
 #pragma unroll
-    for (int k = 0; k < 7; k++) {
+    for (int k = 0; k < 8; k++) {
         u32x4 v = {0u, 0u, 0u, 0u};
 #ifdef DQDK_DIAG_NOHDR  // timing diagnostic only: every lane parses frame 0's header line
         uint64_t o = (a.desc[0].addr & ~15ull) + 16ull * k;
@@ -284,23 +319,53 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
         fi.work |= 1;
     needB = fi.work != 0;
     if (needB) {
-        fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E);
-        if ((fi.work & 2) && fi.g.ct >= 0) {
+        // phase A takes the first line only when all of it lies inside the
+        // UMEM (the bytes it reads are then exactly the stream's)
+        const int a_end = kHeadA && a0 + 128 <= a.umem_size ? 128 - (int)(a0 & 127) : 0;
+        fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E, a_end);
+        const int G = 16 * fi.g.c_begin + fi.g.q4;  // the stream's first byte
+        const int Lc = fi.g.cs_lo;
+        if ((fi.work & 2) && G <= Lc && fi.g.ct >= 0) {
             // head correction: the first streamed chunk starts at G <= cs_lo
             // (4-aligned, G > cs_lo - 16); its bytes before the UDP header are
             // header bytes staged above (cs_lo <= 15 + 14 + 60 < 92)
-            const int G = 16 * fi.g.c_begin + fi.g.q4;
-            const int Lc = fi.g.cs_lo;
-            uint32_t head = 0;
+            fi.head = staged_range_sum(w, G, Lc);
+        } else if (kHeadA && (fi.work & 2) && G > Lc) {
+            // the checksum bytes before the stream were summed here: a
+            // negative head correction (G <= a_end <= 128: all staged)
+            fi.head = 0u - staged_range_sum(w, Lc, min(G, fi.g.cs_hi));
+        }
+        if (kHeadA && (fi.work & 1) && fi.g.de < 0) {
+            // events 0 .. -de-1 lie in chunks before the stream: event k's
+            // chunk is a0-relative dwords s + 4k .. s + 4k + 3 (s = q / 4, 6..24),
+            // aligned here by a 5-step barrel shift (static register indices)
+            na = min((uint32_t)(-fi.g.de), a.E);
+            const int qd = (16 * (fi.g.c_begin + fi.g.de) + fi.g.q4) >> 2;  // s
+            const uint32_t t = (uint32_t)(qd - 6);
+            // (a decoded event's dwords end by a0-relative dword 31: j + t <= 24)
+            constexpr int NX = 4 * kAEv - 1;
+            uint32_t x[NX];
 #pragma unroll
-            for (int k = 0; k < 23; k++) {
-                const int p = 4 * k;
-                uint32_t m = 0;
-                if (p >= G && p < Lc)
-                    m = (Lc - p >= 4) ? 0xffffffffu : ((1u << (8 * (Lc - p))) - 1u);
-                head = __builtin_amdgcn_udot2(as_u16x2(w[k] & m), u16x2{1, 1}, head, false);
+            for (int j = 0; j < NX; j++)
+                x[j] = j + 6 < 32 ? w[j + 6] : 0u;
+#pragma unroll
+            for (int b = 4; b >= 0; b--) {
+                const bool on = (t >> b) & 1u;
+#pragma unroll
+                for (int j = 0; j + (1 << b) < NX; j++)
+                    x[j] = on ? x[j + (1 << b)] : x[j];
             }
-            fi.head = head;
+            const uint32_t rr = (uint32_t)fi.g.r;
+#pragma unroll
+            for (int k = 0; k < kAEv; k++) {
+                const uint32_t xx = __builtin_amdgcn_alignbyte(x[4 * k + 1], x[4 * k], rr);      // event bytes 2..5
+                const uint32_t yy = __builtin_amdgcn_alignbyte(x[4 * k + 2], x[4 * k + 1], rr);  // event bytes 6..9
+                const uint32_t ch = xx & 0xffffu;
+                const uint32_t bin = __builtin_amdgcn_perm(yy, xx, 0x0c0c0403u);
+                const uint32_t hc = __builtin_amdgcn_ubfe(yy, 16, 3);
+                const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;
+                akey[k] = ch < kChannels && hc < kHists ? key : DQDK_KEY_NONE;  // tristan.c:236-241
+            }
         }
     }
 #undef FB
@@ -405,9 +470,9 @@ struct DecodeLds {
 };
 
 // Per-frame stream parameters in the owning lane's VGPRs.
-//   pk1 = nwin | de << 16 | r << 18 | dec << 20 | lw << 21 | th << 22 | tl << 23
+//   pk1 = nwin | (de + 8) << 16 | r << 20 | dec << 22 | lw << 23 | th << 24 | tl << 25
 //   pk2 = tw | mw << 11 | keep << 22
-// nwin: 2-KiB windows; de: chunk of event 0; r: event shift; dec: decode;
+// nwin: 2-KiB windows; de: chunk of event 0 (-7..1); r: event shift; dec: decode;
 // lw: some window needs per-lane checksum weights (chunks past ct), the
 // first such window is mw; tw/tl/th: window/lane/half holding the last
 // checksum chunk when it needs a tail correction (tw = 0xffff: none).
@@ -439,12 +504,12 @@ __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uin
 {
     const uint32_t pk1 = rdl(lf.pk1, j), pk2 = rdl(lf.pk2, j);
     P.nwin = pk1 & 0xffffu;
-    P.de = (pk1 >> 16) & 3u;
-    P.r = (pk1 >> 18) & 3u;
-    P.Ef = (pk1 & (1u << 20)) ? a.E : 0u;
-    P.lw = (pk1 >> 21) & 1u;
-    P.th = (pk1 >> 22) & 1u;
-    P.tl = pk1 >> 23;
+    P.de = ((pk1 >> 16) & 15u) - 8u;  // (u32: e = j - de wraps to j + events phase A took)
+    P.r = (pk1 >> 20) & 3u;
+    P.Ef = (pk1 & (1u << 22)) ? a.E : 0u;
+    P.lw = (pk1 >> 23) & 1u;
+    P.th = (pk1 >> 24) & 1u;
+    P.tl = pk1 >> 25;
     P.tw = pk2 & kNoWin;
     P.mw = (pk2 >> 11) & kNoWin;
     P.keep = (pk2 >> 22) & 31u;
@@ -559,21 +624,25 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const PFrame& P,
 }
 
 // ---- phase A: lane parses frame i and prepares its stream (shared by both decodes) ----
+template <bool kHeadA = false>
 __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, FrameInfo& fi,
-                                        dqdk_gpu_rx_result_t& r, LaneFrame& lf, bool& stream)
+                                        dqdk_gpu_rx_result_t& r, LaneFrame& lf, bool& stream,
+                                        uint32_t (&akey)[kAEv], uint32_t& na)
 {
     bool needB = false;
+    na = 0;
+#pragma unroll
+    for (int k = 0; k < kAEv; k++)
+        akey[k] = DQDK_KEY_NONE;
     if (live)
-        parse_frame(a, i, fi, r, needB);
+        parse_frame<kHeadA>(a, i, fi, r, needB, akey, na);
     stream = false;
     lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
     lf.pk2 = kNoWin | (kNoWin << 11);
     lf.ct = -1;
     if (needB) {
         const Geo& g = fi.g;
-        stream = g.nwin > 0;
-        if (!stream && !udp_csum_ok(0u, fi.check, fi.len16, fi.pseudo))  // empty datagram checksum
-            r.status = DQDK_RX_INVALID_UDP_CSUM;
+        stream = g.nwin > 0;  // (no stream: an empty datagram, or all of it in phase A; phase C checks it)
         const uint64_t boff = (fi.addr & ~15ull) + 16ull * (uint64_t)g.c_begin + (uint64_t)g.q4;
         const uint64_t base = (uint64_t)a.umem + boff;
         const uint64_t ext = 16ull * (uint64_t)g.nch;
@@ -585,8 +654,8 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
         const bool lw = cs && g.ct < g.nch - 1;   // chunks past ct are streamed (decode reaches further)
         const bool tc = cs && g.ct >= 0 && g.keep < 16;
         const uint32_t ct = (uint32_t)(g.ct < 0 ? 0 : g.ct);
-        lf.pk1 = ((uint32_t)g.nwin & 0xffffu) | (((uint32_t)g.de & 3u) << 16) | (((uint32_t)g.r & 3u) << 18) |
-                 ((fi.work & 1u) << 20) | ((lw ? 1u : 0u) << 21) | (((ct >> 6) & 1u) << 22) | ((ct & 63u) << 23);
+        lf.pk1 = ((uint32_t)g.nwin & 0xffffu) | (((uint32_t)(g.de + 8) & 15u) << 16) | (((uint32_t)g.r & 3u) << 20) |
+                 ((fi.work & 1u) << 22) | ((lw ? 1u : 0u) << 23) | (((ct >> 6) & 1u) << 24) | ((ct & 63u) << 25);
         const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
         const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
         lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22);
@@ -616,12 +685,14 @@ __device__ __forceinline__ uint32_t tail_corr(const u32x4& tail, int keep)
 __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, bool stream, const FrameInfo& fi,
                                         dqdk_gpu_rx_result_t& r, uint32_t sum_t, uint32_t sum_oob, const u32x4& tail)
 {
-    if (stream) {
+    if (live) {
         if (fi.work & 2) {
             // tail correction: bytes [keep, 16) of the last checksum chunk lie
             // past the datagram (the odd-length over-read byte is inside keep)
             // (the fused decode subtracted it in the window loop: tail is 0 there)
-            const uint32_t corr = fi.g.ct >= 0 && fi.g.keep < 16 ? tail_corr(tail, fi.g.keep) : 0u;
+            // (no stream: sum_t is 0 and the head correction carries phase A's
+            // sum, or nothing for an empty datagram)
+            const uint32_t corr = stream && fi.g.ct >= 0 && fi.g.keep < 16 ? tail_corr(tail, fi.g.keep) : 0u;
             // udp_csum sums LE words from the UDP start.  tsum summed the words
             // at even addresses: the same words when the UDP header starts at an
             // even address; otherwise every word is byte-swapped, and the one's
@@ -636,7 +707,8 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
             if (!udp_csum_ok(S, fi.check, fi.len16, fi.pseudo))
                 r.status = DQDK_RX_INVALID_UDP_CSUM;
         }
-        // histogram_event's rejections: none without a histogram (E <= 65535, so no clamp)
+        // histogram_event's rejections: none without a histogram (E <= 65535, so no clamp);
+        // sum_oob is 0 for a frame nothing was decoded from
         r.oob_events = (uint16_t)(r.status == DQDK_RX_OK && a.histo ? sum_oob : 0u);
     }
     if (live) {
@@ -668,7 +740,8 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     dqdk_gpu_rx_result_t r;
     LaneFrame lf;
     bool stream;
-    phase_a(a, i, live, fi, r, lf, stream);
+    uint32_t akey[kAEv], na;
+    phase_a(a, i, live, fi, r, lf, stream, akey, na);
 
     // ---- phase B: stream the frames ----
     const uint64_t smask0 = __ballot(stream);
@@ -945,6 +1018,11 @@ __device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uin
     }
 }
 
+// One key phase A decoded (KEY_NONE: out of bounds) into the stage, as
+// fused_chunk does for a streamed event.
+__device__ __forceinline__ void fused_key(const RxArgs& a, uint32_t key, bool has, uint32_t oob_slot, FusedLds& lds,
+                                          __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane);
+
 // Both chunks of a window at once, without divergent branches: every lane
 // issues two returning LDS adds (an event's bucket stage count, a frame's
 // out-of-bounds count, or -- lanes without an event -- a private sink word of
@@ -1015,6 +1093,30 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
         const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
         ovf_put(a, ovf_rsrc, key[0], ov0, base + r0);
         ovf_put(a, ovf_rsrc, key[1], ov1, base + n0 + r1);
+    }
+}
+
+__device__ __forceinline__ void fused_key(const RxArgs& a, uint32_t key, bool has, uint32_t oob_slot, FusedLds& lds,
+                                          __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane)
+{
+    const bool inb = key != DQDK_KEY_NONE;
+    const uint32_t b = min(key >> kL1Shift, (uint32_t)kL1Buckets - 1);
+    uint32_t s = 0;
+    if (has)
+        s = atomicAdd(inb ? &lds.scnt[b] : &lds.oob[oob_slot], kCntUnit);
+    const bool ink = has && inb;
+    if (ink && s < kCntUnit * kFCap)
+        lds.stage[b * kFCap + s / kCntUnit] = key;
+    const bool ov = ink && s >= kCntUnit * kFCap;
+    const uint64_t om = __ballot(ov);
+    if (om) {  // rare: overflow slots, one LDS atomic per wave
+        const uint32_t first = (uint32_t)__builtin_ctzll(om);
+        uint32_t base = 0;
+        if (lane == first)
+            base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
+        base = rdl(base, first);
+        ovf_put(a, ovf_rsrc, key, ov,
+                base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
     }
 }
 
@@ -1125,7 +1227,10 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
 //           the next round completes there);
 //   kLines  flush whole 128-B lines only, carrying each bucket's remainder
 //           (< 32 keys) to the next round: no partial line is ever written.
-template <int kLdAux, bool kLines>
+//   kHeadA  phase A decodes the events (and sums the checksum bytes) of each
+//           frame's first cache line, which it read for the headers; the
+//           stream starts after them (frame_geo's a_end)
+template <int kLdAux, bool kLines, bool kHeadA>
 __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 {
     __shared__ FusedLds lds;
@@ -1160,7 +1265,15 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         dqdk_gpu_rx_result_t r;
         LaneFrame lf;
         bool stream;
-        phase_a(a, i, live, fi, r, lf, stream);
+        uint32_t akey[kAEv], na;
+        phase_a<kHeadA>(a, i, live, fi, r, lf, stream, akey, na);
+        if (kHeadA && __ballot(na != 0)) {
+            // (the stage holds at most the last round's carry here: room for
+            // these keys, at most 7 per frame, is in the round sizing)
+#pragma unroll
+            for (int k = 0; k < kAEv; k++)
+                fused_key(a, akey[k], (uint32_t)k < na, wslot0 + (uint32_t)lane, lds, ovf_rsrc, (uint32_t)lane);
+        }
         const uint64_t smask0 = __ballot(stream);
         const int total = smask0 ? (int)wave_sum_dpp(pk_nwin(lf.pk1)) : 0;
         if (lane == 0)
@@ -1312,10 +1425,14 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
 }
 
-template __global__ void rx_decode_fused_kernel<0, false>(RxArgs);
-template __global__ void rx_decode_fused_kernel<0, true>(RxArgs);
-template __global__ void rx_decode_fused_kernel<2, false>(RxArgs);
-template __global__ void rx_decode_fused_kernel<2, true>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, false, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, true, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, false, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, true, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, false, true>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, true, true>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, false, true>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, true, true>(RxArgs);
 
 // Frames the fused decode staged but whose final status is not OK: subtract
 // their events from the table (u32 wrap: +1 then -1 leaves every bin exact).

@@ -148,8 +148,13 @@ class RxQueue:
                 "async_process_device")
         return int(tot.value)
 
-    def set_raw_fd(self, fd: int) -> None:
-        """Append every host batch's raw payload stream to fd (-1 = off)."""
+    def set_raw_fd(self, fd: int, deferred: bool | None = None) -> None:
+        """Append every host batch's raw payload stream to fd (-1 = off).
+        deferred=True: each batch's write() happens during the next call (or
+        at sync / set_raw_fd / close), overlapped with that batch's kernels;
+        default: written before process_batch returns (tristan.c:318-324)."""
+        if deferred is not None:
+            L.check(L.lib().dqdk_gpu_queue_set_raw_deferred(self._h, int(deferred)), "set_raw_deferred")
         L.check(L.lib().dqdk_gpu_queue_set_raw_fd(self._h, fd), "set_raw_fd")
 
     def register_umem(self, umem: np.ndarray) -> None:

@@ -261,17 +261,24 @@ int dqdk_gpu_fp_fini(uint32_t* host_hist, int csv_fd, dqdk_gpu_counters_t* total
  * with the same d_desc/d_results; writes min(total, out_cap) bytes to d_out
  * (NULL with out_cap 0 = size query).  total (host, nullable) = the stream's
  * full length, which makes the call synchronous.  Host form: with a raw fd
- * set, dqdk_gpu_rx_batch appends each batch's stream to it: the GPU gathers
- * the stream before the call returns (the frames are valid only until the
- * descriptors are released, src/dqdk.c:300), its D2H copy runs on a side
- * stream into one of two pinned buffers, and its write() happens during the
- * next dqdk_gpu_rx_batch call while that batch's kernels run -- or at
- * dqdk_gpu_queue_sync, dqdk_gpu_queue_set_raw_fd and dqdk_gpu_queue_destroy,
- * which drain it.  A failed write() is returned by the call that makes it. */
+ * set, dqdk_gpu_rx_batch appends each batch's stream to it.  By default, as
+ * tristan_process does (src/tristan.c:318-324), the stream is gathered,
+ * copied and write()n before the call returns, and a failed write() is that
+ * call's -errno (returned after the batch's results and delta are
+ * delivered).  Opt-in (dqdk_gpu_queue_set_raw_deferred(q, 1)): the GPU
+ * gathers the stream before the call returns (the frames are valid only
+ * until the descriptors are released, src/dqdk.c:300), its D2H copy runs on
+ * a side stream into one of two pinned buffers, and its write() happens
+ * during the next dqdk_gpu_rx_batch call while that batch's kernels run -- or
+ * at dqdk_gpu_queue_sync, dqdk_gpu_queue_set_raw_fd, set_raw_deferred(q, 0)
+ * and dqdk_gpu_queue_destroy, which drain it.  A failed deferred write() is
+ * returned by the call that makes it (destroy also reports it on stderr): the
+ * caller keeps the fd open until one of those has run. */
 int dqdk_gpu_raw_compact_device(dqdk_gpu_queue_t* q, const uint8_t* d_umem, uint64_t umem_size,
                                 const dqdk_gpu_desc_t* d_desc, uint32_t n, const dqdk_gpu_rx_result_t* d_results,
                                 uint8_t* d_out, uint64_t out_cap, uint64_t* total);
 int dqdk_gpu_queue_set_raw_fd(dqdk_gpu_queue_t* q, int fd); /* -1 = off (default); drains first */
+int dqdk_gpu_queue_set_raw_deferred(dqdk_gpu_queue_t* q, int on); /* 0 = synchronous write() (default) */
 
 /* ---- async consumer (async_processor, src/tristan.c:332-375) --------------- */
 /* The raw/async modes hand each payload to post_async (src/dqdk.c:220-229):

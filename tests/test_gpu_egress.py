@@ -6,12 +6,14 @@ Expected CSV text is produced here with the reference's own format strings
 (header src/tristan.c:198, lines :210 "%d,%d,%u,%u\\n") from the oracle's
 histogram of the same batch, so the file must match byte for byte.
 """
+import ctypes as C
 import os
 
 import numpy as np
 import pytest
 
 import dqdk_amd as D
+from dqdk_amd import _lib as L
 from oracle import oracle as O
 from test_gpu_parity import _need_gpu, run_gpu
 
@@ -286,7 +288,7 @@ def test_raw_stream_side_stream_multi_batch(tmp_path):
     try:
         q = D.RxQueue(0, cfg, max(sizes))
         try:
-            q.set_raw_fd(fd)
+            q.set_raw_fd(fd, deferred=True)
             for b, n in enumerate(sizes):
                 L = 9000 if b % 3 == 1 else 1500
                 umem, desc = D.synth_umem(n, L, 9216, queue=b, faulty=True)
@@ -320,7 +322,7 @@ def test_raw_stream_failed_write_finishes_the_batch_first():
     os.close(r)  # EPIPE on write (Python ignores SIGPIPE)
     q = D.RxQueue(0, cfg, 4096)
     try:
-        q.set_raw_fd(w)
+        q.set_raw_fd(w, deferred=True)
         umem, desc = D.synth_umem(4096, 1500, 4096, queue=0, faulty=True)
         res, _ = q.process_batch(umem, desc)  # batch 0: its write is deferred to the next call
         q.unregister_umem(umem)
@@ -339,3 +341,45 @@ def test_raw_stream_failed_write_finishes_the_batch_first():
     finally:
         q.close()
         os.close(w)
+
+
+def test_raw_stream_synchronous_default_fails_the_same_batch(tmp_path):
+    """The default host raw egress writes each batch before the call returns,
+    as tristan_process does (src/tristan.c:318-324): the file is complete
+    after every call, and a failed write() (EPIPE) is the failing call's own
+    error, with that batch's results delivered and counted.  ADVICE r3 (low)."""
+    _need_gpu()
+    import errno
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM)
+    path = tmp_path / "raw.bin"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    want = []
+    q = D.RxQueue(0, cfg, 4096)
+    try:
+        q.set_raw_fd(fd)
+        for b, n in enumerate([4096, 100]):
+            umem, desc = D.synth_umem(n, 1500, 4096, queue=b, faulty=True)
+            res, _ = q.process_batch(umem, desc)
+            ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+            np.testing.assert_array_equal(res, ores)
+            want.append(ref_raw(umem, desc, ores, ocnt, cfg.flags))
+            q.unregister_umem(umem)
+            assert path.read_bytes() == b"".join(want)  # nothing left in flight
+        r, w = os.pipe()
+        os.close(r)
+        q.set_raw_fd(w)
+        umem, desc = D.synth_umem(2048, 1500, 4096, queue=5, faulty=True)
+        ores, _, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+        per_pkt = np.zeros(len(desc), D.RESULT_DTYPE)
+        delta = L.Counters()
+        rc = L.lib().dqdk_gpu_rx_batch(q._h, umem.ctypes.data, umem.nbytes, desc.ctypes.data, len(desc),
+                                       per_pkt.ctypes.data, C.byref(delta))
+        assert rc == -errno.EPIPE
+        np.testing.assert_array_equal(per_pkt, ores)  # the batch was delivered before the error
+        assert delta.rcvd_pkts == len(desc)
+        q.unregister_umem(umem)
+        q.set_raw_fd(-1)  # nothing pending: no error
+        os.close(w)
+    finally:
+        q.close()
+        os.close(fd)

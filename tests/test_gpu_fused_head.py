@@ -1,0 +1,120 @@
+"""The fused decode's first-line hand-off (fused policy bit 2) vs the oracle.
+
+Phase A reads each frame's first 128 B for the headers; with the hand-off it
+also decodes the events and sums the checksum bytes of that line, and the
+stream starts at the chunk holding the line's end (frame_geo's a_end).  These
+frames exercise every branch of that split: any byte offset (so the line ends
+anywhere from 16 to 128 B past the 16-B aligned start), IP options (ihl 5..15
+move the payload), datagrams that end inside the first line (nothing left to
+stream when few events are decoded), odd lengths, out-of-bounds events in the
+line, bad and absent UDP checksums (the fix-up takes A's keys back), and
+frames whose first line runs past the UMEM end (no hand-off there).  Every
+policy variant runs on the same frames: results, counters and the whole table
+must equal the oracle's.
+"""
+import numpy as np
+import pytest
+
+import dqdk_amd as D
+from oracle import oracle as O
+
+from test_gpu_parity import compare, _need_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _csum16(b: np.ndarray) -> int:
+    """RFC 1071 one's complement sum of big-endian words (odd length: zero pad)."""
+    if b.size & 1:
+        b = np.concatenate([b, np.zeros(1, np.uint8)])
+    w = b.reshape(-1, 2).astype(np.uint32)
+    s = int(((w[:, 0] << 8) | w[:, 1]).sum())
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def build_frames(n: int, seed: int, slot: int = 2048):
+    rng = np.random.default_rng(seed)
+    umem = rng.integers(0, 256, size=n * slot + 512, dtype=np.uint8)
+    desc = np.zeros(n, D.DESC_DTYPE)
+    for i in range(n):
+        a = i * slot + int(rng.integers(0, 256))
+        ihl = 5 if rng.random() < 0.6 else int(rng.integers(5, 16))
+        r = rng.random()
+        dl = int(rng.integers(0, 90)) if r < 0.35 else int(rng.integers(90, 1459)) if r < 0.7 else 1458
+        dl = min(dl, slot - 256 - 14 - 4 * ihl - 8)
+        u = a + 14 + 4 * ihl
+        L = 14 + 4 * ihl + 8 + dl
+        f = umem[a:a + L + 1]
+        f[12], f[13] = 0x08, 0x00
+        f[14] = 0x40 | ihl
+        tot = L - 14
+        f[16], f[17] = tot >> 8, tot & 0xFF
+        f[23] = 17
+        f[24] = f[25] = 0
+        # events: channels mostly in range, classes 0..7 (6, 7 out of range)
+        nev = (L - (u - a) - 8) // 16
+        for e in range(nev):
+            p = u - a + 8 + 16 * e
+            ch = int(rng.integers(0, 1600))
+            f[p + 2], f[p + 3] = ch & 0xFF, ch >> 8
+            f[p + 8] = int(rng.integers(0, 8))
+        c = (~_csum16(f[14:14 + 4 * ihl])) & 0xFFFF
+        f[24], f[25] = c >> 8, c & 0xFF
+        ul = 8 + dl
+        U = u - a
+        f[U + 4], f[U + 5] = ul >> 8, ul & 0xFF
+        f[U + 6] = f[U + 7] = 0
+        if dl & 1 and rng.random() < 0.5:
+            f[U + ul] = 0  # the byte past an odd datagram (read by the reference's sum)
+        pseudo = np.concatenate([f[26:34], np.array([0, 17, ul >> 8, ul & 0xFF], np.uint8)])
+        s = _csum16(np.concatenate([pseudo, f[U:U + ul]]))
+        ck = (~s) & 0xFFFF or 0xFFFF
+        r2 = rng.random()
+        if r2 < 0.1:
+            ck ^= 0x0101  # bad checksum
+        elif r2 < 0.2:
+            ck = 0  # no checksum
+        f[U + 6], f[U + 7] = ck >> 8, ck & 0xFF
+        desc["addr"][i] = a
+        desc["len"][i] = L
+    # the last frames' first lines run past the UMEM end (a0 + 128 > size)
+    size = (int(desc["addr"][-1]) + 40 + 15) // 16 * 16  # (the ABI takes 16-B multiples)
+    desc["len"][-1] = 40
+    desc["addr"][-2] = size - 100
+    desc["len"][-2] = 100
+    return umem[:size].copy(), desc
+
+
+FRAMES = {}
+
+
+def frames(seed):
+    if seed not in FRAMES:
+        FRAMES[seed] = build_frames(3000, seed)
+    return FRAMES[seed]
+
+
+@pytest.mark.parametrize("policy", ["6", "2", "4", "5", "7"])
+@pytest.mark.parametrize("payloadsz", [1458, 48, 16])
+@pytest.mark.parametrize("flags", [D.F_CSUM, 0], ids=["csum", "nocsum"])
+def test_fused_first_line_handoff_vs_oracle(policy, payloadsz, flags, monkeypatch):
+    _need_gpu()
+    monkeypatch.setenv("DQDK_GPU_FUSED_POLICY", policy)
+    umem, desc = frames(31)
+    cfg = D.RxConfig(payloadsz=payloadsz, flags=flags | D.F_HISTO_PARTITIONED)
+    ores, _ = compare(umem, desc, cfg, check_hist=True, records=False)
+    st = ores["status"]
+    assert (st == D.RX_OK).sum() > 1000
+    if flags & D.F_CSUM:
+        assert (st == D.RX_INVALID_UDP_CSUM).sum() > 50  # the fix-up takes staged keys back
+    assert (ores["oob_events"] > 0).sum() > 100
+
+
+def test_builder_frames_pass_the_oracle():
+    """(CPU-side sanity of the builder above, run with the GPU tests.)"""
+    umem, desc = frames(31)
+    ores, _, _ = O.rx_batch(umem.copy(), desc, 1458, 3, D.F_CSUM)
+    ok = ores["status"] == D.RX_OK
+    assert ok.mean() > 0.6, np.unique(ores["status"], return_counts=True)

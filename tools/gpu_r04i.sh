@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 4, call i: the fused decode's first-line hand-off (policy bit 2).
+#   its edge-case parity tests; A/B on one box by DQDK_GPU_FUSED_POLICY
+#   (1500 B: 6 = hand-off vs 2 = round-4 default, twice; 9000 B: 5 vs 1);
+#   PMC traffic passes of the new default at 1500 B; then every GPU test.
+# usage (on the GPU box): bash tools/gpu_r04i.sh <tag>
+set -e
+tag=${1:-r04i}
+mkdir -p gpurun_out
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fused_head.py tests/test_gpu_egress.py -x -q --timeout 120 \
+    --timeout-method thread \
+    > gpurun_out/pytest_${tag}_head.log 2>&1
+b="--no-9000 --no-box-state --no-cpu-baseline"
+for r in 1 2; do
+    for p in 6 2; do
+        DQDK_GPU_FUSED_POLICY=$p timeout -k 10 300 python3 bench.py $b > gpurun_out/ab_${tag}_1500_p${p}_$r.json \
+            2>> gpurun_out/ab_$tag.err
+    done
+done
+for p in 5 1; do
+    DQDK_GPU_FUSED_POLICY=$p timeout -k 10 300 python3 bench.py --frame-len 9000 $b \
+        > gpurun_out/ab_${tag}_9000_p$p.json 2>> gpurun_out/ab_$tag.err
+done
+cp profiles/pmc_summary.json gpurun_out/pmc_summary.json
+bash tools/pmc.sh $tag 1500
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu_$tag.log 2>&1

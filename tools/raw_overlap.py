@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Host drop-in raw egress rate (dqdk_gpu_rx_batch with a raw fd): the serial
-form (gather -> D2H -> write() inside each call, DQDK_GPU_RAW_SYNC=1) against
-the side-stream form (D2H on a side stream, write() of batch b during batch
-b+1's call).  Waveform mode (the raw-storing mode, src/tristan.c:318-324),
+form (gather -> D2H -> write() inside each call, the default) against the
+deferred side-stream form (set_raw_fd(fd, deferred=True): D2H on a side
+stream, write() of batch b during batch b+1's call).  Waveform mode (the raw-storing mode, src/tristan.c:318-324),
 1500 B frames, registered host UMEM, the file in /tmp.  Prints one JSON line."""
 import json
 import os
@@ -16,7 +16,6 @@ import dqdk_amd as D  # noqa: E402
 
 
 def rate(sync: bool, n: int, batches: int, mode: int, sink: str = "file") -> dict:
-    os.environ["DQDK_GPU_RAW_SYNC"] = "1" if sync else "0"
     cfg = D.RxConfig(payloadsz=1458, mode=mode, flags=D.F_CSUM)
     imgs = [D.synth_umem(n, 1500, 4096, queue=k, threads=16) for k in range(2)]
     if sink == "null":
@@ -27,7 +26,7 @@ def rate(sync: bool, n: int, batches: int, mode: int, sink: str = "file") -> dic
         with D.RxQueue(0, cfg, n) as q:
             for u, _ in imgs:
                 q.register_umem(u)
-            q.set_raw_fd(fd)
+            q.set_raw_fd(fd, deferred=not sync)
             q.process_batch(*imgs[0])
             q.sync()
             t0 = time.perf_counter()
@@ -49,7 +48,6 @@ def main():
     n, batches = 1 << 16, 24
     out = {"frames_per_batch": n, "batches": batches, "frame_len": 1500}
     # no raw fd: the host drop-in alone (zero-copy reads of the registered UMEM)
-    os.environ["DQDK_GPU_RAW_SYNC"] = "0"
     imgs = [D.synth_umem(n, 1500, 4096, queue=k, threads=16) for k in range(2)]
     with D.RxQueue(0, D.RxConfig(payloadsz=1458, mode=D.MODE_WAVEFORM, flags=D.F_CSUM), n) as q:
         q.process_batch(*imgs[0])
