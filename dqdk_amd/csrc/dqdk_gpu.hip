@@ -80,6 +80,7 @@ const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",  
                                           "(unused)", "rx_fixup"};
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters, [20] rx_count's ticket
 constexpr int kTicketWord = 20;
+constexpr int kFoldTicketWord = 21;  // the fused decode's folded counters (RxArgs::fold)
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
 {
@@ -176,6 +177,7 @@ struct dqdk_gpu_queue {
     uint32_t* d_snap = nullptr;    // u32 snapshot for histogram_device_ptr (lazy)
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
+    uint32_t* d_blkcnt = nullptr;  // fused decode: per-block folded counters (kMaxFusedGrid x kFoldWords)
     uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
     uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
     uint64_t part1_elems = 0;
@@ -487,6 +489,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
 }
 
 bool small_off();
+bool fold_off();
 
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
@@ -552,6 +555,14 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.ovf_blk = q->d_ovf_blk;
         ra.ovf_blk_cap = q->ovf_cap_blk;
         ra.hist = q->d_hist;
+        // per-packet counters in the decode itself (the host drop-in's
+        // publishing batches keep rx_count, which writes its pinned results)
+        ra.fold = !q->publish && !fold_off();
+        ra.blk_cnt = q->d_blkcnt;
+        ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
+        ra.cum = q->d_cum;
+        if (grid > (uint32_t)kMaxFusedGrid)
+            return fail_errno(-EINVAL, "fused decode: grid exceeds the folded-counter blocks");
         if ((uint64_t)ra.ovf_blk_cap * grid > q->ovf_blk_elems)
             return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
         StageTimer t(q, kStDecode);
@@ -583,7 +594,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     HIPCHK(hipGetLastError());
 
-    if (fused || n > (uint32_t)kTile || small_off()) {
+    if (fused ? !ra.fold : (n > (uint32_t)kTile || small_off())) {
         const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
         {
             StageTimer t(q, kStAbort);
@@ -605,6 +616,13 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (q->histo && q->E)
         return launch_histo(q, n, d_res, keys, partitioned, fused ? &fg : nullptr, ra, slot_scratch);
     return 0;
+}
+
+// DQDK_GPU_FOLD=0: the fused path counts in rx_abort + rx_count launches (A/B only)
+bool fold_off()
+{
+    const char* v = getenv("DQDK_GPU_FOLD");
+    return v && !strcmp(v, "0");
 }
 
 // DQDK_GPU_SMALL=0: small batches take the three-launch form too (A/B only)
@@ -913,7 +931,8 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMalloc(&q->d_batch, kBatchScratch * sizeof(uint64_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_desc, (size_t)max_batch * sizeof(dqdk_gpu_desc_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess ||
-        (e = hipMalloc(&q->d_raw_blk, ((size_t)max_batch / kRawThreads + 2) * sizeof(uint64_t))) != hipSuccess)
+        (e = hipMalloc(&q->d_raw_blk, ((size_t)max_batch / kRawThreads + 2) * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMalloc(&q->d_blkcnt, (size_t)kMaxFusedGrid * kFoldWords * sizeof(uint32_t))) != hipSuccess)
         return cleanup((fail("hipMalloc", e), -ENOMEM));
     if ((e = hipMemset(q->d_cum, 0, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
@@ -1071,6 +1090,7 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     dev_free(q->d_snap);
     (void)hipFree(q->d_cum);
     (void)hipFree(q->d_batch);
+    (void)hipFree(q->d_blkcnt);
     dev_free(q->d_keys);
     dev_free(q->d_part1);
     dev_free(q->d_part1_rec);

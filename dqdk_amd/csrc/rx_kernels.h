@@ -184,7 +184,16 @@ struct RxArgs {
     uint32_t round_windows;   // windows per wave per round (multiple of the ring depth)
     uint32_t tile_frames;     // records path: frames per wave tile (0 = 64; fewer spread a small
                               //   batch over more waves, the host drop-in's zero-copy frames)
+    // fused path, counters folded into the decode (no rx_abort / rx_count
+    // launches; per-packet accounting only): per-block partial sums
+    // (kFoldWords u32 each), the last block by ticket writes the batch's
+    // [first abort idx, counters] to batch_scratch and adds them to cum
+    uint32_t fold;
+    uint32_t* blk_cnt;
+    uint32_t* ticket;         // zero between launches
+    dqdk_gpu_counters_t* cum;
 };
+constexpr int kFoldWords = 16;
 
 struct CountArgs {
     const dqdk_gpu_rx_result_t* res;

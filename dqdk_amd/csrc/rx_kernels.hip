@@ -946,7 +946,112 @@ struct FusedLds {
 #endif
     uint32_t wtot[kFWaves];          // windows of each wave's tile
     uint32_t ovf_n;                  // keys in this block's private overflow region
+    alignas(8) uint32_t fc[kFoldWords];  // folded counters of the block (FoldWord; the bytes word pair is a u64)
 };
+
+// Folded counters (RxArgs::fold): the block's sums of rx_count's per-frame
+// accounting (src/dqdk.c:252-322 per-packet form), in LDS then blk_cnt.
+enum FoldWord { F_FILT, F_FRAMES, F_IP, F_UDP, F_EMPTY, F_OK, F_BYTES_LO, F_BYTES_HI, F_OOB, F_FAIL, F_NWORDS };
+
+// One wave's frames of a super-tile into the block's folded counters
+// (ballots and DPP sums; lane 0 adds to LDS).  i0: the frame index of lane 0.
+__device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool live, const dqdk_gpu_rx_result_t& r,
+                                            uint32_t i0, int lane)
+{
+    const uint32_t st = r.status;
+    const bool inb = st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
+    const bool ok = live && st == DQDK_RX_OK;
+    const uint64_t mfail = __ballot(live && inb && st != DQDK_RX_OK);
+    const uint32_t filt = (uint32_t)__builtin_popcountll(__ballot(live && !inb));
+    const uint32_t frames = (uint32_t)__builtin_popcountll(__ballot(live && inb));
+    const uint32_t ip = (uint32_t)__builtin_popcountll(
+        __ballot(live && (st == DQDK_RX_INVALID_IP || st == DQDK_RX_INVALID_IP_CSUM)));
+    const uint32_t udp = (uint32_t)__builtin_popcountll(
+        __ballot(live && (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM)));
+    const uint32_t empty = (uint32_t)__builtin_popcountll(__ballot(live && st == DQDK_RX_EMPTY));
+    const uint32_t nok = (uint32_t)__builtin_popcountll(__ballot(ok));
+    const uint32_t bytes = wave_sum_dpp(ok ? r.datalen : 0u);  // (64 x 65535 < 2^32)
+    const uint32_t oob = wave_sum_dpp(ok && a.histo ? (uint32_t)r.oob_events : 0u);
+    if (lane == 0) {
+        if (filt)
+            atomicAdd(&lds.fc[F_FILT], filt);
+        if (frames)
+            atomicAdd(&lds.fc[F_FRAMES], frames);
+        if (ip)
+            atomicAdd(&lds.fc[F_IP], ip);
+        if (udp)
+            atomicAdd(&lds.fc[F_UDP], udp);
+        if (empty)
+            atomicAdd(&lds.fc[F_EMPTY], empty);
+        if (nok)
+            atomicAdd(&lds.fc[F_OK], nok);
+        if (bytes)
+            atomicAdd((unsigned long long*)&lds.fc[F_BYTES_LO], (unsigned long long)bytes);
+        if (oob)
+            atomicAdd(&lds.fc[F_OOB], oob);
+        if (mfail)
+            atomicMin(&lds.fc[F_FAIL], i0 + (uint32_t)__builtin_ctzll(mfail));
+    }
+}
+
+// The block's folded counters to blk_cnt; the last block (ticket) sums every
+// block's and publishes the batch: batch_scratch [0] = first failing frame
+// (n: none), [1..12] = dqdk_gpu_counters_t of the batch, each added to cum
+// -- what rx_abort + rx_count write for a per-packet batch (count_block).
+__device__ __forceinline__ void fold_publish(const RxArgs& a, FusedLds& lds, int tid)
+{
+    __shared__ uint32_t last;
+    __shared__ uint64_t tot[F_NWORDS];
+    __syncthreads();  // every wave's fold_frames adds are in LDS
+    if (tid < F_NWORDS)
+        a.blk_cnt[blockIdx.x * kFoldWords + tid] = lds.fc[tid];
+    __threadfence();
+    __syncthreads();
+    if (tid == 0)
+        last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last)
+        return;  // (block-uniform)
+    __threadfence();
+    const int lane = tid & 63, wave = tid >> 6;
+    if (wave < F_NWORDS && wave != F_BYTES_HI) {
+        // wave k sums word k of every block (F_BYTES_LO: the u64 of words 6, 7)
+        const bool mn = wave == F_FAIL;
+        uint64_t v = mn ? ~0ull : 0ull;
+        for (uint32_t b = (uint32_t)lane; b < gridDim.x; b += 64) {
+            const uint32_t* w = a.blk_cnt + b * kFoldWords;
+            uint64_t x = __hip_atomic_load(&w[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wave == F_BYTES_LO)
+                x |= (uint64_t)__hip_atomic_load(&w[F_BYTES_HI], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
+            v = mn ? (x < v ? x : v) : v + x;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t y = __shfl_xor(v, o);
+            v = mn ? (y < v ? y : v) : v + y;
+        }
+        if (lane == 0)
+            tot[wave] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint64_t n = a.n;
+        const uint64_t fail = tot[F_FAIL] < n ? tot[F_FAIL] : n;
+        const uint64_t c[12] = {tot[F_FRAMES], tot[F_FRAMES], tot[F_BYTES_LO], tot[F_IP],
+                                tot[F_UDP],    fail < n ? 1ull : 0ull, tot[F_OK] * a.E, tot[F_BYTES_LO],
+                                tot[F_OOB],    tot[F_EMPTY], tot[F_FILT], fail};
+        unsigned long long* cum = (unsigned long long*)a.cum;
+        a.batch_scratch[0] = fail;
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            a.batch_scratch[1 + k] = c[k];
+            if (k < 11 && c[k])
+                atomicAdd(&cum[k], (unsigned long long)c[k]);
+        }
+        cum[11] = fail;  // first_abort_idx of this batch
+        *a.ticket = 0;
+    }
+}
 
 // Block barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release + acquire: on gfx950 that is s_waitcnt vmcnt(0) before s_barrier,
@@ -1244,6 +1349,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     lds.oob[tid] = 0;
     if (tid == 0)
         lds.ovf_n = 0;
+    if (tid < kFoldWords)
+        lds.fc[tid] = tid == F_FAIL ? ~0u : 0u;
     __syncthreads();
     // this block's private overflow region (ovf_blk_cap keys, then the table)
     uint32_t* const ovf_blk = a.ovf_blk + (uint64_t)blockIdx.x * a.ovf_blk_cap;
@@ -1392,6 +1499,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 #else
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
 #endif
+        if (a.fold)
+            fold_frames(a, lds, live, r, tile * 64u, lane);
         // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
         if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
             a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
@@ -1423,6 +1532,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (tid < kL1Buckets && lds.scnt[tid])
             atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
+    if (a.fold)
+        fold_publish(a, lds, tid);
 }
 
 template __global__ void rx_decode_fused_kernel<0, false, false>(RxArgs);

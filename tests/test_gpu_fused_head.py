@@ -118,3 +118,33 @@ def test_builder_frames_pass_the_oracle():
     ores, _, _ = O.rx_batch(umem.copy(), desc, 1458, 3, D.F_CSUM)
     ok = ores["status"] == D.RX_OK
     assert ok.mean() > 0.6, np.unique(ores["status"], return_counts=True)
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("flags", [D.F_CSUM, D.F_CSUM | D.F_PREFILTER, 0], ids=["csum", "prefilter", "nocsum"])
+def test_folded_counters_vs_oracle(fold, flags, monkeypatch):
+    """The fused decode counts per-packet batches itself (per-block sums, the
+    last block publishes; DQDK_GPU_FOLD=0: rx_abort + rx_count launches):
+    every counter, cumulated over two batches, equals the oracle's."""
+    _need_gpu()
+    monkeypatch.setenv("DQDK_GPU_FOLD", fold)
+    umem, desc = frames(31)
+    cfg = D.RxConfig(payloadsz=1458, flags=flags | D.F_HISTO_PARTITIONED, port_start=0, port_end=65535)
+    ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags, cfg.port_start, cfg.port_end)
+    q = D.RxQueue(0, cfg, len(desc))
+    try:
+        import torch
+        d_umem = torch.from_numpy(umem).to("cuda:0")
+        d_desc = torch.from_numpy(desc.view(np.uint8)).to("cuda:0")
+        d_res = torch.empty(len(desc) * 8, dtype=torch.uint8, device="cuda:0")
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        for _ in range(2):
+            q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), len(desc), d_res.data_ptr(), None)
+        torch.cuda.synchronize()
+        got = q.counters()
+    finally:
+        q.close()
+    for k, v in ocnt.items():
+        want = v if k == "first_abort_idx" else 2 * v
+        assert got[k] == want, (k, got[k], want)
+    assert ocnt["invalid_udp_pkts"] > 0 and ocnt["first_abort_idx"] < len(desc)

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round 4, call i: the fused decode's first-line hand-off (policy bit 2).
-#   its edge-case parity tests; A/B on one box by DQDK_GPU_FUSED_POLICY
-#   (1500 B: 6 = hand-off vs 2 = round-4 default, twice; 9000 B: 5 vs 1);
+#   its edge-case parity tests and the folded counters'; A/B on one box by
+#   DQDK_GPU_FUSED_POLICY / DQDK_GPU_FOLD (1500 B: 6 = hand-off vs 2 =
+#   round-4 default, folded counters vs rx_abort + rx_count, twice; 9000 B:
+#   5 vs 1);
 #   PMC traffic passes of the new default at 1500 B; then every GPU test.
 # usage (on the GPU box): bash tools/gpu_r04i.sh <tag>
 set -e
@@ -12,9 +14,10 @@ timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fused_head.py tests/test_g
     > gpurun_out/pytest_${tag}_head.log 2>&1
 b="--no-9000 --no-box-state --no-cpu-baseline"
 for r in 1 2; do
-    for p in 6 2; do
-        DQDK_GPU_FUSED_POLICY=$p timeout -k 10 300 python3 bench.py $b > gpurun_out/ab_${tag}_1500_p${p}_$r.json \
-            2>> gpurun_out/ab_$tag.err
+    for v in "6 1" "2 1" "6 0"; do
+        set -- $v
+        DQDK_GPU_FUSED_POLICY=$1 DQDK_GPU_FOLD=$2 timeout -k 10 300 python3 bench.py $b \
+            > gpurun_out/ab_${tag}_1500_p$1_f$2_$r.json 2>> gpurun_out/ab_$tag.err
     done
 done
 for p in 5 1; do
