@@ -490,6 +490,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
 
 bool small_off();
 bool fold_off();
+uint32_t frame_map();
 
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
@@ -558,6 +559,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         // per-packet counters in the decode itself (the host drop-in's
         // publishing batches keep rx_count, which writes its pinned results)
         ra.fold = !q->publish && !fold_off();
+        ra.fmap = frame_map();
         ra.blk_cnt = q->d_blkcnt;
         ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
         ra.cum = q->d_cum;
@@ -623,6 +625,18 @@ bool fold_off()
 {
     const char* v = getenv("DQDK_GPU_FOLD");
     return v && !strcmp(v, "0");
+}
+
+// The fused decode's frame map: 0 = each wave streams 64 consecutive
+// frames, 1 = a block's waves stream 16 adjacent frames at a time
+// (DQDK_GPU_FRAME_MAP overrides per batch)
+#ifndef DQDK_FRAME_MAP
+#define DQDK_FRAME_MAP 0u
+#endif
+uint32_t frame_map()
+{
+    const char* v = getenv("DQDK_GPU_FRAME_MAP");
+    return v && *v ? (uint32_t)(atoi(v) != 0) : (uint32_t)(DQDK_FRAME_MAP);
 }
 
 // DQDK_GPU_SMALL=0: small batches take the three-launch form too (A/B only)

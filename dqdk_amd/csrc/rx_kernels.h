@@ -189,6 +189,7 @@ struct RxArgs {
     // (kFoldWords u32 each), the last block by ticket writes the batch's
     // [first abort idx, counters] to batch_scratch and adds them to cum
     uint32_t fold;
+    uint32_t fmap;            // fused: 1 = interleaved frame map (see rx_decode_fused_kernel)
     uint32_t* blk_cnt;
     uint32_t* ticket;         // zero between launches
     dqdk_gpu_counters_t* cum;

@@ -954,14 +954,21 @@ struct FusedLds {
 enum FoldWord { F_FILT, F_FRAMES, F_IP, F_UDP, F_EMPTY, F_OK, F_BYTES_LO, F_BYTES_HI, F_OOB, F_FAIL, F_NWORDS };
 
 // One wave's frames of a super-tile into the block's folded counters
-// (ballots and DPP sums; lane 0 adds to LDS).  i0: the frame index of lane 0.
+// (ballots and DPP sums; lane 0 adds to LDS).  i: the lane's frame index.
 __device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool live, const dqdk_gpu_rx_result_t& r,
-                                            uint32_t i0, int lane)
+                                            uint32_t i, int lane)
 {
     const uint32_t st = r.status;
     const bool inb = st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
     const bool ok = live && st == DQDK_RX_OK;
-    const uint64_t mfail = __ballot(live && inb && st != DQDK_RX_OK);
+    const bool fail = live && inb && st != DQDK_RX_OK;
+    const uint64_t mfail = __ballot(fail);
+    uint32_t ifail = fail ? i : ~0u;  // the wave's first failing frame
+    if (mfail) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            ifail = min(ifail, (uint32_t)__shfl_xor((int)ifail, o));
+    }
     const uint32_t filt = (uint32_t)__builtin_popcountll(__ballot(live && !inb));
     const uint32_t frames = (uint32_t)__builtin_popcountll(__ballot(live && inb));
     const uint32_t ip = (uint32_t)__builtin_popcountll(
@@ -990,7 +997,7 @@ __device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool
         if (oob)
             atomicAdd(&lds.fc[F_OOB], oob);
         if (mfail)
-            atomicMin(&lds.fc[F_FAIL], i0 + (uint32_t)__builtin_ctzll(mfail));
+            atomicMin(&lds.fc[F_FAIL], ifail);
     }
 }
 
@@ -1364,8 +1371,11 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
         const uint32_t tile = st * kFWaves + wave;
-        const uint32_t i = tile * 64 + (uint32_t)lane;
-        const bool live = tile < ntiles && i < a.n;
+        // frame of this lane: tile-major (64 consecutive frames per wave), or
+        // interleaved (a.fmap: the block's waves stream 16 adjacent frames at
+        // a time -- lane l of wave w takes frame 1024 st + 16 l + w)
+        const uint32_t i = a.fmap ? st * (64u * kFWaves) + (uint32_t)lane * kFWaves + wave : tile * 64 + (uint32_t)lane;
+        const bool live = i < a.n;
 
         // ---- phase A ----
         FrameInfo fi;
@@ -1500,7 +1510,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
 #endif
         if (a.fold)
-            fold_frames(a, lds, live, r, tile * 64u, lane);
+            fold_frames(a, lds, live, r, i, lane);
         // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
         if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
             a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;

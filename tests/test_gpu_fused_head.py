@@ -148,3 +148,19 @@ def test_folded_counters_vs_oracle(fold, flags, monkeypatch):
         want = v if k == "first_abort_idx" else 2 * v
         assert got[k] == want, (k, got[k], want)
     assert ocnt["invalid_udp_pkts"] > 0 and ocnt["first_abort_idx"] < len(desc)
+
+
+@pytest.mark.parametrize("policy", ["6", "1"])
+@pytest.mark.parametrize("fmap", ["1", "0"])
+def test_frame_maps_vs_oracle(policy, fmap, monkeypatch):
+    """Both frame maps of the fused decode (tile-major: a wave streams 64
+    consecutive frames; interleaved: a block's waves stream 16 adjacent
+    frames at a time), with the folded counters: results, counters (first
+    failing frame included) and table equal the oracle's."""
+    _need_gpu()
+    monkeypatch.setenv("DQDK_GPU_FUSED_POLICY", policy)
+    monkeypatch.setenv("DQDK_GPU_FRAME_MAP", fmap)
+    umem, desc = frames(31)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
+    ores, ocnt = compare(umem, desc, cfg, check_hist=True, records=False)
+    assert ocnt["first_abort_idx"] < len(desc)
