@@ -1980,7 +1980,10 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArg
 // back by the block): lds_barrier() keeps the next item's key loads in flight
 // across them.
 template <int kLdAux>
-__global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
+#ifndef DQDK_P2_WAVES  // waves per SIMD the register budget is cut for (8: two blocks per CU, 64 VGPRs)
+#define DQDK_P2_WAVES 8
+#endif
+__global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(HistoArgs a)  // 32 waves per CU
 {
     constexpr int kMaxSeg = kL1Buckets * kSegsPerBucket;
     constexpr int kPWaves = kPartThreads / 64;
@@ -2082,6 +2085,12 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
     // (a gathered item's triple j loads into key[2j], key[2j + 1] and is
     // unpacked in place, from the last triple down)
     uint32_t key[kPartKeysPerThread];
+#ifndef DQDK_P2_RREG  // 1: the ranks stay in registers from count() to scatter() (A/B)
+#define DQDK_P2_RREG 0
+#endif
+#if DQDK_P2_RREG
+    uint32_t rr[kRankWords];
+#endif
     uint32_t pad = 0;  // gathered: bit 2j + i set = key 3j + 2 - i is a pad of its piece's last triple
     auto load = [&](const Item& g, int pb) {
         pad = 0;
@@ -2193,7 +2202,12 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             }
 #pragma unroll
             for (int j = 0; j < kH / 2; j++)
+#if DQDK_P2_RREG
+                if (h / 2 + j < kRankWords)
+                    rr[h / 2 + j] = r[2 * j] | (r[2 * j + 1] << 16);
+#else
                 rnk[(h / 2 + j) * kPartThreads + tid] = r[2 * j] | (r[2 * j + 1] << 16);
+#endif
         }
     };
     // scatter: each key's u16 to its slice run in the stage, at the run start
@@ -2206,7 +2220,11 @@ __global__ void __launch_bounds__(kPartThreads, 8) rx_part2_kernel(HistoArgs a) 
             uint32_t o[8], rk[4];
 #pragma unroll
             for (int j = 0; j < 4; j++)
+#if DQDK_P2_RREG
+                rk[j] = h / 2 + j < kRankWords ? rr[h / 2 + j] : 0u;
+#else
                 rk[j] = rnk[(h / 2 + j) * kPartThreads + tid];
+#endif
 #pragma unroll
             for (int j = 0; j < 8; j++)
                 if (h + j < kPartKeysPerThread)
