@@ -147,7 +147,9 @@ def test_folded_counters_vs_oracle(fold, flags, monkeypatch):
     for k, v in ocnt.items():
         want = v if k == "first_abort_idx" else 2 * v
         assert got[k] == want, (k, got[k], want)
-    assert ocnt["invalid_udp_pkts"] > 0 and ocnt["first_abort_idx"] < len(desc)
+    assert ocnt["first_abort_idx"] < len(desc)
+    if flags & D.F_CSUM:
+        assert ocnt["invalid_udp_pkts"] > 0
 
 
 @pytest.mark.parametrize("policy", ["6", "1"])
