@@ -177,7 +177,7 @@ struct dqdk_gpu_queue {
     uint32_t* d_snap = nullptr;    // u32 snapshot for histogram_device_ptr (lazy)
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
-    uint32_t* d_blkcnt = nullptr;  // fused decode: per-block folded counters (kMaxFusedGrid x kFoldWords)
+    uint32_t* d_blkcnt = nullptr;  // fused decode: the folded counters' accumulators (kFoldWords u64)
     uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
     uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
     uint64_t part1_elems = 0;
@@ -563,8 +563,6 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.blk_cnt = q->d_blkcnt;
         ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
         ra.cum = q->d_cum;
-        if (grid > (uint32_t)kMaxFusedGrid)
-            return fail_errno(-EINVAL, "fused decode: grid exceeds the folded-counter blocks");
         if ((uint64_t)ra.ovf_blk_cap * grid > q->ovf_blk_elems)
             return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
         StageTimer t(q, kStDecode);
@@ -946,8 +944,14 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMalloc(&q->d_desc, (size_t)max_batch * sizeof(dqdk_gpu_desc_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_res, (size_t)max_batch * sizeof(dqdk_gpu_rx_result_t))) != hipSuccess ||
         (e = hipMalloc(&q->d_raw_blk, ((size_t)max_batch / kRawThreads + 2) * sizeof(uint64_t))) != hipSuccess ||
-        (e = hipMalloc(&q->d_blkcnt, (size_t)kMaxFusedGrid * kFoldWords * sizeof(uint32_t))) != hipSuccess)
+        (e = hipMalloc(&q->d_blkcnt, kFoldWords * sizeof(uint64_t))) != hipSuccess)
         return cleanup((fail("hipMalloc", e), -ENOMEM));
+    {
+        uint64_t acc0[kFoldWords] = {};
+        acc0[9] = ~0ull;  // the first-failure accumulator (FoldWord F_FAIL)
+        if ((e = hipMemcpy(q->d_blkcnt, acc0, sizeof(acc0), hipMemcpyHostToDevice)) != hipSuccess)
+            return cleanup(fail("hipMemcpy", e));
+    }
     if ((e = hipMemset(q->d_cum, 0, sizeof(dqdk_gpu_counters_t))) != hipSuccess ||
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));

@@ -185,9 +185,10 @@ struct RxArgs {
     uint32_t tile_frames;     // records path: frames per wave tile (0 = 64; fewer spread a small
                               //   batch over more waves, the host drop-in's zero-copy frames)
     // fused path, counters folded into the decode (no rx_abort / rx_count
-    // launches; per-packet accounting only): per-block partial sums
-    // (kFoldWords u32 each), the last block by ticket writes the batch's
-    // [first abort idx, counters] to batch_scratch and adds them to cum
+    // launches; per-packet accounting only): the batch's accumulators
+    // (kFoldWords u64, zero but the first-failure word, all ones, between
+    // launches), the last block by ticket writes the batch's [first abort
+    // idx, counters] to batch_scratch and adds them to cum
     uint32_t fold;
     uint32_t fmap;            // fused: 1 = interleaved frame map (see rx_decode_fused_kernel)
     uint32_t* blk_cnt;

@@ -95,8 +95,10 @@ __device__ __forceinline__ Geo frame_geo(uint32_t work, uint32_t off0, uint32_t 
 
 // Per-frame hand-off from phase A (lane per frame) to phase B (wave per frame).
 struct FrameInfo {
-    uint64_t addr;
-    uint64_t pseudo;   // saddr + daddr + ((17 + len16) << 8), csum_tcpudp_nofold terms
+    uint64_t addr;     // (phase A only: phase C re-reads the descriptor for the write-back)
+    uint32_t pseudo;   // saddr + daddr + ((17 + len16) << 8), the csum_tcpudp_nofold terms, folded to
+                       //   32 bits (end-around carry: the same value mod 0xffff, all the verdict uses)
+    uint8_t odd;       // the UDP header starts at an odd address
     uint32_t datalen;
     uint16_t len16;    // (u16)udplen handed to udp_audit_checksum
     uint16_t check;    // udp->check as stored (LE u16)
@@ -162,7 +164,7 @@ __device__ __forceinline__ uint32_t staged_range_sum(const uint32_t (&w)[32], in
 // ---------------------------------------------------------------------------
 template <bool kHeadA>
 __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameInfo& fi, dqdk_gpu_rx_result_t& r,
-                                            bool& needB, uint32_t (&akey)[kAEv], uint32_t& na)
+                                            bool& needB, uint32_t (&akey)[kAEv], uint32_t& na, uint32_t& hw, bool& sh)
 {
     dqdk_gpu_desc_t d = a.desc[i];
     const uint64_t addr = d.addr;
@@ -170,6 +172,8 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
     const uint64_t a0 = addr & ~15ull;
     const uint32_t off0 = (uint32_t)(addr & 15);
     na = 0;
+    hw = 0;
+    sh = false;
 
     // 8 aligned chunks = 128 B from a0: covers frame bytes [0, 113) for any off0
     // (the headers need [0, 97)).
@@ -206,6 +210,7 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
     r.oob_events = 0;
     fi.addr = addr;
     fi.pseudo = 0;
+    fi.odd = 0;
     fi.datalen = 0;
     fi.len16 = 0;
     fi.check = 0;
@@ -310,7 +315,11 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
         const uint32_t len16 = udplen & 0xffffu;
         fi.len16 = (uint16_t)len16;
         fi.check = (uint16_t)ucheck;
-        fi.pseudo = (uint64_t)saddr + (uint64_t)daddr + (uint64_t)(uint32_t)((17u + len16) << 8);
+        uint64_t ps = (uint64_t)saddr + (uint64_t)daddr + (uint64_t)(uint32_t)((17u + len16) << 8);
+        ps = (ps & 0xffffffffull) + (ps >> 32);  // from64to32 (2^32 = 1 mod 0xffff)
+        ps = (ps & 0xffffffffull) + (ps >> 32);
+        fi.pseudo = (uint32_t)ps;
+        fi.odd = (uint8_t)((addr + 14 + hs) & 1);
         fi.work |= 2;
     }
     // events are decoded only for a consumer: the histogram (histo_fd > 0,
@@ -323,6 +332,25 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
         // UMEM (the bytes it reads are then exactly the stream's)
         const int a_end = kHeadA && a0 + 128 <= a.umem_size ? 128 - (int)(a0 & 127) : 0;
         fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E, a_end);
+        if (kHeadA && a_end > 0 && fi.g.nch > 0) {
+            // The stream's first chunk may begin up to 12 B before the line
+            // ends (the chunk grid is the events'): phase B would then fetch
+            // the whole line again for those bytes (the L2 fetches 128-B
+            // lines).  One such dword comes from here instead (sh: lane 0 of
+            // the frame's first window loads 4 B further and shifts this dword
+            // in); with more, the frame keeps the round-3 geometry.
+            const int G0 = 16 * fi.g.c_begin + fi.g.q4;
+            if (G0 < a_end) {
+                if (a_end - G0 == 4 && fi.g.nch >= 2 && a0 + (uint64_t)G0 + 20 <= a.umem_size) {
+                    sh = true;
+#pragma unroll
+                    for (int k = 0; k < 32; k++)
+                        hw = k == (G0 >> 2) ? w[k] : hw;
+                } else {
+                    fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E, 0);
+                }
+            }
+        }
         const int G = 16 * fi.g.c_begin + fi.g.q4;  // the stream's first byte
         const int Lc = fi.g.cs_lo;
         if ((fi.work & 2) && G <= Lc && fi.g.ct >= 0) {
@@ -471,8 +499,9 @@ struct DecodeLds {
 
 // Per-frame stream parameters in the owning lane's VGPRs.
 //   pk1 = nwin | (de + 8) << 16 | r << 20 | dec << 22 | lw << 23 | th << 24 | tl << 25
-//   pk2 = tw | mw << 11 | keep << 22
+//   pk2 = tw | mw << 11 | keep << 22 | sh << 27
 // nwin: 2-KiB windows; de: chunk of event 0 (-7..1); r: event shift; dec: decode;
+// sh: the first chunk's first dword comes from phase A (fused, parse_frame);
 // lw: some window needs per-lane checksum weights (chunks past ct), the
 // first such window is mw; tw/tl/th: window/lane/half holding the last
 // checksum chunk when it needs a tail correction (tw = 0xffff: none).
@@ -498,6 +527,7 @@ struct PFrame {
     uint32_t nwin, de, r, Ef, lw, th, tl, tw, mw;  // Ef = events to decode (0: frame not decoded)
     int ct;
     uint32_t keep;  // checksum bytes in the last checksum chunk (tail correction when < 16)
+    uint32_t sh, hw;  // fused first-line hand-off: lane 0's first chunk starts with hw
 };
 
 __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uint32_t j, PFrame& P)
@@ -513,6 +543,8 @@ __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uin
     P.tw = pk2 & kNoWin;
     P.mw = (pk2 >> 11) & kNoWin;
     P.keep = (pk2 >> 22) & 31u;
+    P.sh = (pk2 >> 27) & 1u;
+    P.hw = 0;
     P.ct = P.lw ? (int)rdl((uint32_t)lf.ct, j) : 0;
 }
 
@@ -627,15 +659,16 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const PFrame& P,
 template <bool kHeadA = false>
 __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, FrameInfo& fi,
                                         dqdk_gpu_rx_result_t& r, LaneFrame& lf, bool& stream,
-                                        uint32_t (&akey)[kAEv], uint32_t& na)
+                                        uint32_t (&akey)[kAEv], uint32_t& na, uint32_t& hw)
 {
-    bool needB = false;
+    bool needB = false, sh = false;
     na = 0;
+    hw = 0;
 #pragma unroll
     for (int k = 0; k < kAEv; k++)
         akey[k] = DQDK_KEY_NONE;
     if (live)
-        parse_frame<kHeadA>(a, i, fi, r, needB, akey, na);
+        parse_frame<kHeadA>(a, i, fi, r, needB, akey, na, hw, sh);
     stream = false;
     lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
     lf.pk2 = kNoWin | (kNoWin << 11);
@@ -658,7 +691,7 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
                  ((fi.work & 1u) << 22) | ((lw ? 1u : 0u) << 23) | (((ct >> 6) & 1u) << 24) | ((ct & 63u) << 25);
         const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
         const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
-        lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22);
+        lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22) | ((sh && stream ? 1u : 0u) << 27);
         lf.ct = g.ct;
     }
     if (!stream)
@@ -700,7 +733,7 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
             // mod 0xffff is all udp_csum_ok depends on; + 0xffff keeps the
             // check subtraction from wrapping)
             const uint32_t tsum = sum_t - fi.head - corr;
-            const bool even = ((fi.addr + 14 + fi.hs) & 1) == 0;
+            const bool even = !fi.odd;
             uint32_t f = (tsum & 0xffffu) + (tsum >> 16);
             f = (f & 0xffffu) + (f >> 16);
             const uint32_t S = even ? tsum : (((f >> 8) | (f << 8)) & 0xffffu) + 0xffffu;
@@ -718,7 +751,7 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
         }
         a.res[i] = r;
         if ((fi.work & 2) && (a.flags & DQDK_GPU_F_CSUM_WRITEBACK)) {  // udp.c:17 side effect
-            const uint64_t ck = fi.addr + 14 + fi.hs + 6;
+            const uint64_t ck = a.desc[i].addr + 14 + fi.hs + 6;
             if (ck + 2 <= a.umem_size) {
                 uint8_t* p = const_cast<uint8_t*>(a.umem) + ck;
                 p[0] = 0;
@@ -740,8 +773,8 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     dqdk_gpu_rx_result_t r;
     LaneFrame lf;
     bool stream;
-    uint32_t akey[kAEv], na;
-    phase_a(a, i, live, fi, r, lf, stream, akey, na);
+    uint32_t akey[kAEv], na, hw;
+    phase_a(a, i, live, fi, r, lf, stream, akey, na, hw);
 
     // ---- phase B: stream the frames ----
     const uint64_t smask0 = __ballot(stream);
@@ -977,7 +1010,10 @@ __device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool
         __ballot(live && (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM)));
     const uint32_t empty = (uint32_t)__builtin_popcountll(__ballot(live && st == DQDK_RX_EMPTY));
     const uint32_t nok = (uint32_t)__builtin_popcountll(__ballot(ok));
-    const uint32_t bytes = wave_sum_dpp(ok ? r.datalen : 0u);  // (64 x 65535 < 2^32)
+    // datalen is a u32 that wraps to ~4 G for udplen < 8 (dqdk.c:205): the
+    // wave sums its 16-bit halves (64 x 65535 < 2^32 each)
+    const uint32_t dl = ok ? r.datalen : 0u;
+    const uint64_t bytes = (uint64_t)wave_sum_dpp(dl & 0xffffu) + ((uint64_t)wave_sum_dpp(dl >> 16) << 16);
     const uint32_t oob = wave_sum_dpp(ok && a.histo ? (uint32_t)r.oob_events : 0u);
     if (lane == 0) {
         if (filt)
@@ -993,7 +1029,7 @@ __device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool
         if (nok)
             atomicAdd(&lds.fc[F_OK], nok);
         if (bytes)
-            atomicAdd((unsigned long long*)&lds.fc[F_BYTES_LO], (unsigned long long)bytes);
+            atomicAdd((unsigned long long*)&lds.fc[F_BYTES_LO], (unsigned long long)bytes);  // (u64 per block)
         if (oob)
             atomicAdd(&lds.fc[F_OOB], oob);
         if (mfail)
@@ -1001,45 +1037,35 @@ __device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool
     }
 }
 
-// The block's folded counters to blk_cnt; the last block (ticket) sums every
-// block's and publishes the batch: batch_scratch [0] = first failing frame
-// (n: none), [1..12] = dqdk_gpu_counters_t of the batch, each added to cum
-// -- what rx_abort + rx_count write for a per-packet batch (count_block).
+// The block's folded counters into the batch's accumulators (a.blk_cnt as
+// u64 words: device atomics, which execute at the memory side, so no fence
+// and no L2 write-back -- an agent-scope fence here wrote back every XCD's
+// dirty piece lines under the still-running blocks: decode +0.1 ms); the
+// last block (ticket, taken once its own adds have returned) swaps the
+// totals out, resetting them, and publishes the batch: batch_scratch [0] =
+// first failing frame (n: none), [1..12] = dqdk_gpu_counters_t of the batch,
+// each added to cum -- what rx_abort + rx_count write for a per-packet batch.
 __device__ __forceinline__ void fold_publish(const RxArgs& a, FusedLds& lds, int tid)
 {
     __shared__ uint32_t last;
     __shared__ uint64_t tot[F_NWORDS];
+    unsigned long long* acc = (unsigned long long*)a.blk_cnt;  // [F_NWORDS] (F_BYTES_HI unused)
     __syncthreads();  // every wave's fold_frames adds are in LDS
-    if (tid < F_NWORDS)
-        a.blk_cnt[blockIdx.x * kFoldWords + tid] = lds.fc[tid];
-    __threadfence();
-    __syncthreads();
-    if (tid == 0)
-        last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    if (tid < 64) {
+        uint64_t r = 0;
+        if (tid < F_NWORDS && tid != F_BYTES_HI) {
+            const uint64_t v = tid == F_BYTES_LO ? *(const uint64_t*)&lds.fc[F_BYTES_LO] : (uint64_t)lds.fc[tid];
+            r = tid == F_FAIL ? atomicMin(&acc[F_FAIL], (unsigned long long)v) : atomicAdd(&acc[tid], (unsigned long long)v);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(r) : "memory");  // the adds are performed before the ticket
+        if (tid == 0)
+            last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    }
     __syncthreads();
     if (!last)
         return;  // (block-uniform)
-    __threadfence();
-    const int lane = tid & 63, wave = tid >> 6;
-    if (wave < F_NWORDS && wave != F_BYTES_HI) {
-        // wave k sums word k of every block (F_BYTES_LO: the u64 of words 6, 7)
-        const bool mn = wave == F_FAIL;
-        uint64_t v = mn ? ~0ull : 0ull;
-        for (uint32_t b = (uint32_t)lane; b < gridDim.x; b += 64) {
-            const uint32_t* w = a.blk_cnt + b * kFoldWords;
-            uint64_t x = __hip_atomic_load(&w[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (wave == F_BYTES_LO)
-                x |= (uint64_t)__hip_atomic_load(&w[F_BYTES_HI], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
-            v = mn ? (x < v ? x : v) : v + x;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t y = __shfl_xor(v, o);
-            v = mn ? (y < v ? y : v) : v + y;
-        }
-        if (lane == 0)
-            tot[wave] = v;
-    }
+    if (tid < F_NWORDS && tid != F_BYTES_HI)
+        tot[tid] = atomicExch(&acc[tid], tid == F_FAIL ? ~0ull : 0ull);  // the totals; reset for the next batch
     __syncthreads();
     if (tid == 0) {
         const uint64_t n = a.n;
@@ -1382,8 +1408,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         dqdk_gpu_rx_result_t r;
         LaneFrame lf;
         bool stream;
-        uint32_t akey[kAEv], na;
-        phase_a<kHeadA>(a, i, live, fi, r, lf, stream, akey, na);
+        uint32_t akey[kAEv], na, hw;
+        phase_a<kHeadA>(a, i, live, fi, r, lf, stream, akey, na, hw);
+        if (kHeadA && ((lf.pk2 >> 27) & 1u))
+            lds.sum[wslot0 + (uint32_t)lane] = hw;  // (to phase B through the frame's sum slot, see pfr)
         if (kHeadA && __ballot(na != 0)) {
             // (the stage holds at most the last round's carry here: room for
             // these keys, at most 7 per frame, is in the round sizing)
@@ -1409,10 +1437,14 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         uint32_t jl = smask0 ? (uint32_t)__builtin_ctzll(lmask) : 0u;
         uint32_t wl = 0, lnwin = smask0 ? pk_nwin(rdl(lf.pk1, jl)) : 0u;
         __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
+        // (kHeadA) lane 0 of a sh frame's first window loads 4 B further: its
+        // chunk's first dword lies in the line phase A read (see pfr)
+        const uint32_t lsh_lane = kHeadA && lane == 0 ? 4u : 0u;
+        uint32_t lsh = kHeadA && smask0 ? (rdl(lf.pk2, jl) >> 27) & 1u : 0u;
         auto issue = [&](u32x4& d0, u32x4& d1) {
-            const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes : kOOB);
+            const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes + (wl == 0 && lsh ? lsh_lane : 0u) : kOOB);
             d0 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo, 0, kLdAux);
-            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u, 0, kLdAux);
+            d1 = __builtin_amdgcn_raw_buffer_load_b128(lrs, vo + 1024u - (wl == 0 && lsh ? lsh_lane : 0u), 0, kLdAux);
             if (lmask != 0 && ++wl == lnwin) {
                 wl = 0;
                 lmask &= lmask - 1;
@@ -1420,6 +1452,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                     jl = (uint32_t)__builtin_ctzll(lmask);
                     lnwin = pk_nwin(rdl(lf.pk1, jl));
                     lrs = frame_rsrc(lf, jl);
+                    if (kHeadA)
+                        lsh = (rdl(lf.pk2, jl) >> 27) & 1u;
                 }
             }
         };
@@ -1431,8 +1465,19 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         uint32_t jp = smask0 ? (uint32_t)__builtin_ctzll(pmask) : 0u;
         uint32_t wp = 0;
         PFrame P;
+        // a frame's stream parameters; a sh frame's first dword from its
+        // sum slot, which phase A used to hand it over (reset before the
+        // frame's sum reaches it)
+        auto pfr = [&](uint32_t j) {
+            pframe(a, lf, j, P);
+            if (kHeadA && P.sh) {
+                P.hw = lds.sum[wslot0 + j];
+                if (lane == 0)
+                    lds.sum[wslot0 + j] = 0;
+            }
+        };
         if (smask0)
-            pframe(a, lf, jp, P);
+            pfr(jp);
         else
             P = PFrame{0, 0, 0, 0, 0, 0, 0, kNoWin, kNoWin, 0, 16};
         uint32_t acc0 = 0, acc1 = 0;
@@ -1445,6 +1490,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             for (int d = 0; d < kFRingW; d++) {
                 const bool active = k + d < total;
                 const uint32_t jw = (uint32_t)kWinChunks * wp;
+                if (kHeadA && active && wp == 0 && P.sh && lane == 0)  // the frame's first chunk: hw + 12 loaded bytes
+                    b0[d] = u32x4{P.hw, b0[d].x, b0[d].y, b0[d].z};
                 if (active && wp >= P.mw) {
                     const int j0 = (int)jw + lane;
                     csum_pair(b0[d], b1[d], j0 <= P.ct ? u16x2{1, 1} : u16x2{0, 0},
@@ -1483,7 +1530,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                     pmask &= pmask - 1;
                     if (pmask) {
                         jp = (uint32_t)__builtin_ctzll(pmask);
-                        pframe(a, lf, jp, P);
+                        pfr(jp);
                     }
                 }
                 issue(b0[d], b1[d]);

@@ -14,13 +14,13 @@ timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fused_head.py tests/test_g
     > gpurun_out/pytest_${tag}_head.log 2>&1
 b="--no-9000 --no-box-state --no-cpu-baseline"
 for r in 1 2; do
-    for v in "6 1 0" "2 1 0" "6 0 0" "6 1 1"; do
+    for v in "6 1 0" "2 1 0" "6 0 0" "2 0 0"; do
         set -- $v
         DQDK_GPU_FUSED_POLICY=$1 DQDK_GPU_FOLD=$2 DQDK_GPU_FRAME_MAP=$3 timeout -k 10 300 python3 bench.py $b \
             > gpurun_out/ab_${tag}_1500_p$1_f$2_m$3_$r.json 2>> gpurun_out/ab_$tag.err
     done
 done
-for v in "5 0" "1 0" "1 1"; do
+for v in "5 0" "1 0"; do
     set -- $v
     DQDK_GPU_FUSED_POLICY=$1 DQDK_GPU_FRAME_MAP=$2 timeout -k 10 300 python3 bench.py --frame-len 9000 $b \
         > gpurun_out/ab_${tag}_9000_p$1_m$2.json 2>> gpurun_out/ab_$tag.err
