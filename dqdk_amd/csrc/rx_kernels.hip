@@ -341,7 +341,10 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
             // in); with more, the frame keeps the round-3 geometry.
             const int G0 = 16 * fi.g.c_begin + fi.g.q4;
             if (G0 < a_end) {
-                if (a_end - G0 == 4 && fi.g.nch >= 2 && a0 + (uint64_t)G0 + 20 <= a.umem_size) {
+                // (the dword travels in LaneFrame::ct, unused unless chunks past
+                // the checksum are streamed: such frames keep the old geometry)
+                const bool lw = (fi.work & 2) && fi.g.ct < fi.g.nch - 1;
+                if (a_end - G0 == 4 && !lw && fi.g.nch >= 2 && a0 + (uint64_t)G0 + 20 <= a.umem_size) {
                     sh = true;
 #pragma unroll
                     for (int k = 0; k < 32; k++)
@@ -544,7 +547,7 @@ __device__ __forceinline__ void pframe(const RxArgs& a, const LaneFrame& lf, uin
     P.mw = (pk2 >> 11) & kNoWin;
     P.keep = (pk2 >> 22) & 31u;
     P.sh = (pk2 >> 27) & 1u;
-    P.hw = 0;
+    P.hw = P.sh ? rdl((uint32_t)lf.ct, j) : 0u;
     P.ct = P.lw ? (int)rdl((uint32_t)lf.ct, j) : 0;
 }
 
@@ -691,8 +694,11 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
                  ((fi.work & 1u) << 22) | ((lw ? 1u : 0u) << 23) | (((ct >> 6) & 1u) << 24) | ((ct & 63u) << 25);
         const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
         const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
+#ifdef DQDK_DIAG_SHNONE  // timing diagnostic only: the hand-off geometry without the register dword (phase B reads it)
+        sh = false;
+#endif
         lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22) | ((sh && stream ? 1u : 0u) << 27);
-        lf.ct = g.ct;
+        lf.ct = sh ? (int)hw : g.ct;  // (sh frames never need ct: see parse_frame)
     }
     if (!stream)
         lf.pk1 = 0;
@@ -1410,8 +1416,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         bool stream;
         uint32_t akey[kAEv], na, hw;
         phase_a<kHeadA>(a, i, live, fi, r, lf, stream, akey, na, hw);
-        if (kHeadA && ((lf.pk2 >> 27) & 1u))
-            lds.sum[wslot0 + (uint32_t)lane] = hw;  // (to phase B through the frame's sum slot, see pfr)
+        (void)hw;
         if (kHeadA && __ballot(na != 0)) {
             // (the stage holds at most the last round's carry here: room for
             // these keys, at most 7 per frame, is in the round sizing)
@@ -1438,8 +1443,12 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         uint32_t wl = 0, lnwin = smask0 ? pk_nwin(rdl(lf.pk1, jl)) : 0u;
         __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
         // (kHeadA) lane 0 of a sh frame's first window loads 4 B further: its
-        // chunk's first dword lies in the line phase A read (see pfr)
+        // chunk's first dword lies in the line phase A read (PFrame::hw)
+#ifdef DQDK_DIAG_SHLOAD0  // timing diagnostic only: lane 0 loads at the grid offset (wrong bytes)
+        const uint32_t lsh_lane = 0u;
+#else
         const uint32_t lsh_lane = kHeadA && lane == 0 ? 4u : 0u;
+#endif
         uint32_t lsh = kHeadA && smask0 ? (rdl(lf.pk2, jl) >> 27) & 1u : 0u;
         auto issue = [&](u32x4& d0, u32x4& d1) {
             const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes + (wl == 0 && lsh ? lsh_lane : 0u) : kOOB);
@@ -1465,17 +1474,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         uint32_t jp = smask0 ? (uint32_t)__builtin_ctzll(pmask) : 0u;
         uint32_t wp = 0;
         PFrame P;
-        // a frame's stream parameters; a sh frame's first dword from its
-        // sum slot, which phase A used to hand it over (reset before the
-        // frame's sum reaches it)
-        auto pfr = [&](uint32_t j) {
-            pframe(a, lf, j, P);
-            if (kHeadA && P.sh) {
-                P.hw = lds.sum[wslot0 + j];
-                if (lane == 0)
-                    lds.sum[wslot0 + j] = 0;
-            }
-        };
+        auto pfr = [&](uint32_t j) { pframe(a, lf, j, P); };
         if (smask0)
             pfr(jp);
         else
