@@ -346,9 +346,14 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
                 const bool lw = (fi.work & 2) && fi.g.ct < fi.g.nch - 1;
                 if (a_end - G0 == 4 && !lw && fi.g.nch >= 2 && a0 + (uint64_t)G0 + 20 <= a.umem_size) {
                     sh = true;
-#pragma unroll
-                    for (int k = 0; k < 32; k++)
-                        hw = k == (G0 >> 2) ? w[k] : hw;
+                    // the dword at G0 = a_end - 4: w[31 - 4m], m = (a0 & 127) / 16
+                    // (a select tree: a compare-select over all 32 registers
+                    // had the compiler emit 8K more instructions in phase A)
+                    const uint32_t m = (uint32_t)(a0 & 127) >> 4;
+                    const uint32_t h01 = (m & 1) ? w[27] : w[31], h23 = (m & 1) ? w[19] : w[23];
+                    const uint32_t h45 = (m & 1) ? w[11] : w[15], h67 = (m & 1) ? w[3] : w[7];
+                    const uint32_t h03 = (m & 2) ? h23 : h01, h47 = (m & 2) ? h67 : h45;
+                    hw = (m & 4) ? h47 : h03;
                 } else {
                     fi.g = frame_geo(fi.work, off0, fi.poff, hs, fi.len16, a.E, 0);
                 }
