@@ -344,12 +344,13 @@ int hist_flush(dqdk_gpu_queue* q)
 // and remainders carried, which costs stage room, hence the smaller round
 // (A/B, one box, 9000 B: decode 2.86 -> 2.44 ms; at 1500 B lines cost 0.04 ms).
 // policy bit 0: whole-line flushes, bit 1: non-temporal frame loads, bit 2:
-// phase A takes each frame's first line (events and checksum bytes; its room
-// in the stage is the round sizing's margin, so only with triples flushes,
-// whose carry is at most 2 keys per bucket).  DQDK_GPU_FUSED_POLICY=<0..7>
-// overrides it per batch (A/B on one box; the tests run every variant).
+// phase A takes each frame's first line (events and checksum bytes; phase B
+// then never touches that line: traffic 2.08 -> 1.96 GB at 1M x 1500 B, but
+// the decode 0.432 -> 0.455 ms on one box, r04k2: the extra phase-A work
+// costs more than the line, so it is off by default).  DQDK_GPU_FUSED_POLICY
+// =<0..7> overrides it per batch (A/B on one box; the tests run every variant).
 #ifndef DQDK_FUSED_POLICY
-#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 6u)
+#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 2u)
 #endif
 uint32_t fused_policy(uint32_t E)
 {
