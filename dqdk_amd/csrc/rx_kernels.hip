@@ -1167,11 +1167,6 @@ __device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uin
     }
 }
 
-// One key phase A decoded (KEY_NONE: out of bounds) into the stage, as
-// fused_chunk does for a streamed event.
-__device__ __forceinline__ void fused_key(const RxArgs& a, uint32_t key, bool has, uint32_t oob_slot, FusedLds& lds,
-                                          __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane);
-
 // Both chunks of a window at once, without divergent branches: every lane
 // issues two returning LDS adds (an event's bucket stage count, a frame's
 // out-of-bounds count, or -- lanes without an event -- a private sink word of
@@ -1245,27 +1240,47 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     }
 }
 
-__device__ __forceinline__ void fused_key(const RxArgs& a, uint32_t key, bool has, uint32_t oob_slot, FusedLds& lds,
-                                          __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane)
+// Phase A's keys (akey[0, na), KEY_NONE: out of bounds) into the stage, as
+// fused_pair stages a window's: every returning LDS add first (lanes with
+// no key add to their sink word), one wait, then the stores, then one
+// ballot for the rare overflow -- one LDS round trip, not kAEv.
+__device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&akey)[kAEv], uint32_t na,
+                                             uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc,
+                                             uint32_t lane)
 {
-    const bool inb = key != DQDK_KEY_NONE;
-    const uint32_t b = min(key >> kL1Shift, (uint32_t)kL1Buckets - 1);
-    uint32_t s = 0;
-    if (has)
-        s = atomicAdd(inb ? &lds.scnt[b] : &lds.oob[oob_slot], kCntUnit);
-    const bool ink = has && inb;
-    if (ink && s < kCntUnit * kFCap)
-        lds.stage[b * kFCap + s / kCntUnit] = key;
-    const bool ov = ink && s >= kCntUnit * kFCap;
-    const uint64_t om = __ballot(ov);
-    if (om) {  // rare: overflow slots, one LDS atomic per wave
-        const uint32_t first = (uint32_t)__builtin_ctzll(om);
-        uint32_t base = 0;
-        if (lane == first)
-            base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
-        base = rdl(base, first);
-        ovf_put(a, ovf_rsrc, key, ov,
-                base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
+    uint32_t* const sink = &lds.stage[kL1Buckets * kFCap + lane];
+    uint32_t sl[kAEv];
+#pragma unroll
+    for (int k = 0; k < kAEv; k++) {
+        const bool has = (uint32_t)k < na, inb = akey[k] != DQDK_KEY_NONE;
+        const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
+        sl[k] = atomicAdd(has ? (inb ? &lds.scnt[b] : &lds.oob[oob_slot]) : sink, kCntUnit);
+    }
+    bool anyov = false;
+#pragma unroll
+    for (int k = 0; k < kAEv; k++) {
+        const bool ink = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE;
+        const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
+        const bool st = ink && sl[k] < kCntUnit * kFCap;
+        *(st ? &lds.stage[b * kFCap + sl[k] / kCntUnit] : sink) = akey[k];
+        anyov |= ink && !st;
+    }
+    if (__ballot(anyov)) {  // rare: overflow slots
+#pragma unroll
+        for (int k = 0; k < kAEv; k++) {
+            const bool ov = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE && sl[k] >= kCntUnit * kFCap;
+            const uint64_t om = __ballot(ov);
+            if (om) {
+                const uint32_t first = (uint32_t)__builtin_ctzll(om);
+                uint32_t base = 0;
+                if (lane == first)
+                    base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
+                base = rdl(base, first);
+                ovf_put(a, ovf_rsrc, akey[k], ov,
+                        base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
+            }
+        }
     }
 }
 
@@ -1425,9 +1440,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (kHeadA && __ballot(na != 0)) {
             // (the stage holds at most the last round's carry here: room for
             // these keys, at most 7 per frame, is in the round sizing)
-#pragma unroll
-            for (int k = 0; k < kAEv; k++)
-                fused_key(a, akey[k], (uint32_t)k < na, wslot0 + (uint32_t)lane, lds, ovf_rsrc, (uint32_t)lane);
+#ifndef DQDK_DIAG_NOASTAGE  // timing diagnostic only: phase A's keys dropped
+            fused_keys_a(a, akey, na, wslot0 + (uint32_t)lane, lds, ovf_rsrc, (uint32_t)lane);
+#endif
         }
         const uint64_t smask0 = __ballot(stream);
         const int total = smask0 ? (int)wave_sum_dpp(pk_nwin(lf.pk1)) : 0;
