@@ -81,6 +81,7 @@ const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",  
 constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch counters, [20] rx_count's ticket
 constexpr int kTicketWord = 20;
 constexpr int kFoldTicketWord = 21;  // the fused decode's folded counters (RxArgs::fold)
+constexpr int kPart2TicketWord = 22;  // rx_part2's last block re-zeroes the slot's counters
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
 {
@@ -187,6 +188,10 @@ struct dqdk_gpu_queue {
     uint16_t* d_part2 = nullptr;
     uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
     uint32_t* d_hscratch = nullptr;
+    // staged slots whose per-batch counters (scratch [0, kZeroWords)) are not
+    // known to be zero: set until a batch's rx_part2 (which re-zeroes them
+    // at its end) is enqueued on the slot, memset on the next use otherwise
+    std::vector<uint8_t> slot_dirty;
     uint32_t* d_fix = nullptr;     // fused path: decoded frames that failed afterwards (max_batch)
     uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions (in d_part1's rx_part1 region)
     uint64_t ovf_blk_elems = 0;    // grid * ovf_cap_blk
@@ -475,6 +480,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     }
     if (q->publish && fused)  // rx_fixup was the last reader of the caller's frames
         HIPCHK(hipEventRecord(q->ev_read, q->stream));
+    ha.p2_ticket = (uint32_t*)(q->d_batch + kPart2TicketWord);
     {
         StageTimer t(q, kStPart2);
         // non-temporal key loads where the fused decode's are (fused_policy bit 1)
@@ -484,6 +490,8 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
             hipLaunchKernelGGL(rx_part2_kernel<0>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
     }
     HIPCHK(hipGetLastError());
+    if (q->hist_pending < q->slot_dirty.size())
+        q->slot_dirty[q->hist_pending] = 0;  // re-zeroed by this rx_part2's last block
     if (++q->hist_pending == q->hist_k)
         return hist_flush(q);
     return 0;
@@ -492,6 +500,21 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
 bool small_off();
 bool fold_off();
 uint32_t frame_map();
+bool part2_zero_off();
+
+// The staged slot's per-batch counters are zero before its batch's first
+// kernel: a memset only when the slot's last rx_part2 did not re-zero them
+// (first use, or a batch that failed on the way); dirty until this batch's
+// rx_part2 is enqueued.
+int clean_slot(dqdk_gpu_queue* q, uint32_t* slot_scratch)
+{
+    if (q->slot_dirty.size() < q->hist_k)
+        q->slot_dirty.resize(q->hist_k, 1);
+    if (q->slot_dirty[q->hist_pending] || part2_zero_off())
+        HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+    q->slot_dirty[q->hist_pending] = 1;
+    return 0;
+}
 
 int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, const dqdk_gpu_desc_t* d_desc,
                  uint32_t n, dqdk_gpu_rx_result_t* d_res, uint32_t* d_keys)
@@ -526,7 +549,8 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     uint32_t* slot_scratch = q->d_hscratch + (size_t)q->hist_pending * q->scratch_words;
     ra.cnt1 = partitioned && !fused ? slot_scratch + kOffCnt1 : nullptr;
     if (partitioned)
-        HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+        if (int rc = clean_slot(q, slot_scratch))
+            return rc;
 
     CountArgs ca{};
     ca.res = d_res;
@@ -638,6 +662,13 @@ uint32_t frame_map()
     return v && *v ? (uint32_t)(atoi(v) != 0) : (uint32_t)(DQDK_FRAME_MAP);
 }
 
+// DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch (A/B only)
+bool part2_zero_off()
+{
+    const char* v = getenv("DQDK_GPU_P2ZERO");
+    return v && !strcmp(v, "0");
+}
+
 // DQDK_GPU_SMALL=0: small batches take the three-launch form too (A/B only)
 bool small_off()
 {
@@ -658,7 +689,8 @@ int launch_payloads(dqdk_gpu_queue* q, const uint8_t* d_stage, const uint32_t* d
     uint32_t* slot_scratch =
         q->d_hscratch ? q->d_hscratch + (size_t)q->hist_pending * q->scratch_words : nullptr;
     if (partitioned)
-        HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+        if (int rc = clean_slot(q, slot_scratch))
+            return rc;
     if (histo) {
         if (int rc = ensure_records(q, true, partitioned))
             return rc;

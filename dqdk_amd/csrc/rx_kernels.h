@@ -240,6 +240,10 @@ struct HistoArgs {
     uint32_t nslots;
     uint32_t scratch_stride;
     uint64_t part2_stride, runs_stride;
+    // rx_part2: the last block (ticket, zero between launches) re-zeroes
+    // scratch [0, kZeroWords), the per-batch counters, once every block has
+    // read them: the slot is clean for its next batch without a memset
+    uint32_t* p2_ticket;
 };
 
 // Frame-processor plugin (dqdk_gpu_frame_processor, frame_processor.hip):

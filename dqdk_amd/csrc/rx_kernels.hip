@@ -2358,6 +2358,23 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         // (no barrier here: the stage and s_nv are rewritten only after the
         // next item's first barrier)
     }
+    if (a.p2_ticket) {
+        // every block read the counters in its prologue: the last one to
+        // finish zeroes them for the slot's next batch (device atomics and
+        // the zeroing stores are ordered by the kernel boundary for the
+        // kernels that follow on the stream)
+        __shared__ uint32_t p2_last;
+        __syncthreads();
+        if (tid == 0)
+            p2_last = atomicAdd(a.p2_ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (p2_last) {
+            for (int w = tid; w < kZeroWords; w += kPartThreads)
+                a.scratch[w] = 0u;
+            if (tid == 0)
+                *a.p2_ticket = 0u;
+        }
+    }
 }
 
 template __global__ void rx_part2_kernel<0>(HistoArgs);
