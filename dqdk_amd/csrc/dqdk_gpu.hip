@@ -369,7 +369,10 @@ uint32_t fused_round_windows(uint32_t E)
 #ifndef DQDK_FUSED_FILL  // (134-key stage: W = 16 at 1500 B, 12 at 9000 B; A/B r04g: 20 / 16 slower)
 #define DQDK_FUSED_FILL (E >= 128 ? 65 : 61)
 #endif
-    const uint32_t w = (uint32_t)(DQDK_FUSED_FILL / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
+    double fill = DQDK_FUSED_FILL;
+    if (const char* v = getenv("DQDK_GPU_FUSED_FILL"))  // (A/B only: stage fill target in percent)
+        fill = atof(v);
+    const uint32_t w = (uint32_t)(fill / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth
     return std::max<uint32_t>(kFRingW, std::min<uint32_t>(64, wr));
 }
