@@ -402,7 +402,8 @@ def box_state(torch, dev_index):
     """The GPU box's memory-system state, recorded in the bench line from this
     process (the decode runs in one of two per-box speed states):
     the device's current clock levels (gfx / memory / fabric / SoC), compute
-    and memory partition modes, performance level and temperatures, read from
+    and memory partition modes, performance level, HBM vendor, VBIOS and
+    product identity, PCIe link, and temperatures, read from
     the amdgpu sysfs files of the HIP device's own PCI function (plain
     read-only file reads; no SMI tool is started), or the error that
     prevented it."""
@@ -427,9 +428,12 @@ def box_state(torch, dev_index):
             t = rd(f"pp_dpm_{clk}")
             out[f"{clk}_current"] = current(t)
             out[f"{clk}_levels"] = t.replace("\n", "; ")
+        # (the HBM vendor and firmware identity: candidates for what tells the
+        # speed states apart, which the clocks and partitions do not)
         for f in ("current_compute_partition", "current_memory_partition", "power_dpm_force_performance_level",
-                  "mem_info_vram_total", "mem_info_vram_used"):
-            out[f] = rd(f)
+                  "mem_info_vram_total", "mem_info_vram_used", "mem_info_vram_vendor", "vbios_version",
+                  "product_name", "current_link_speed", "current_link_width"):
+            out[f] = rd(f, 200)
         temps = {}
         for hw in sorted((base / "hwmon").glob("hwmon*")):
             for t in sorted(hw.glob("temp*_input")):
