@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Where the per-process 9000 B speed state lives: in one
+process, several device UMEM images holding the same frames (each its own
+contiguous allocation, plus one from torch's allocator) decoded by several
+queues (each with its own staging allocations), every (image, queue) pair
+timed interleaved.  If the decode time follows the image or the queue within
+one process, the state is the placement of that allocation; if every pair
+runs alike and only processes differ, it is process-wide.  Prints one JSON
+line.
+
+usage: python tools/state_probe.py [--frames 1048576] [--frame-len 9000] [--images 3] [--queues 2] [--reps 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import bench  # noqa: E402  (its synthetic-UMEM helpers)
+import dqdk_amd as D  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--frame-len", type=int, default=9000)
+    ap.add_argument("--images", type=int, default=3)
+    ap.add_argument("--queues", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=6)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    L, n = args.frame_len, args.frames
+    stride = 4096 if L <= 4096 else 9216
+    size = bench.umem_size(D, n, L, stride, 0)
+    bufs = [D.DeviceBuffer(0, size) for _ in range(args.images)]  # images first, as bench.py does
+    d0, d_desc, desc, _, _ = bench.synth_to_device(D, torch, dev, n, L, stride, 0, image=bufs[0])
+    imgs = [("contig0", bufs[0], d0)]
+    for k in range(1, args.images):
+        t = bufs[k].tensor[:size]
+        t.copy_(d0)
+        imgs.append((f"contig{k}", bufs[k], t))
+    tt = torch.empty(size, dtype=torch.uint8, device=dev)
+    tt.copy_(d0)
+    imgs.append(("torch", None, tt))
+    cfg = D.RxConfig(payloadsz=L - 42, flags=D.F_CSUM)
+    stream = torch.cuda.current_stream(dev)
+    queues = []
+    for _ in range(args.queues):
+        q = D.RxQueue(0, cfg, n)
+        q.set_stream(stream.cuda_stream)
+        queues.append(q)
+    d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
+    times = {}
+    for rep in range(args.reps):
+        for qi, q in enumerate(queues):
+            for name, _, t in imgs:
+                for _ in range(2):  # warm
+                    q.process_device(t.data_ptr(), size, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+                torch.cuda.synchronize(dev)
+                q.read_timing()
+                q.timing_stages(["rx_decode"])
+                q.enable_timing(True)
+                for _ in range(args.steps):
+                    q.process_device(t.data_ptr(), size, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+                torch.cuda.synchronize(dev)
+                q.enable_timing(False)
+                s = q.read_timing()["rx_decode"]
+                times.setdefault(f"q{qi}/{name}", []).append(round(s["ms"] / s["launches"], 4))
+    out = {"frame_len": L, "frames": n, "decode_ms": times,
+           "va_mod_2MiB": {name: (t.data_ptr() % (2 << 20)) for name, _, t in imgs}}
+    print(json.dumps(out), flush=True)
+    for q in queues:
+        q.close()
+    for b in bufs:
+        b.close()
+
+
+if __name__ == "__main__":
+    main()
