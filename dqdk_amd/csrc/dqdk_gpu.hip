@@ -82,6 +82,9 @@ constexpr int kBatchScratch = 32;  // u64 words: [0] abort idx, [1..12] batch co
 constexpr int kTicketWord = 20;
 constexpr int kFoldTicketWord = 21;  // the fused decode's folded counters (RxArgs::fold)
 constexpr int kPart2TicketWord = 22;  // rx_part2's last block re-zeroes the slot's counters
+// The fused pieces' offset inside their allocation can move by up to this
+// many words (placement relative to the frames: DESIGN.md §5)
+constexpr uint64_t kPieceShiftMax = 8u << 20;  // 32 MiB
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
 {
@@ -182,6 +185,7 @@ struct dqdk_gpu_queue {
     uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
     uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
     uint64_t part1_elems = 0;
+    uint64_t piece_shift = 0;      // fused pieces start this many words into d_part1 (< kPieceShiftMax)
     uint32_t* d_part1_rec = nullptr;  // records path: rx_part1's output when d_part1 is smaller (first use)
     uint32_t* d_ovf = nullptr;     // fused path: the overflow list (ovf_blk_elems keys)
     uint32_t ovf_cap_blk = 0;      // fused path: keys per block overflow region
@@ -397,6 +401,15 @@ int ensure_records(dqdk_gpu_queue* q, bool keys, bool part1)
     return 0;
 }
 
+// The fused pieces' offset in words; DQDK_GPU_PIECE_SHIFT (KiB) overrides it
+// per batch (A/B and tools/state_probe.py)
+uint64_t piece_shift(const dqdk_gpu_queue* q)
+{
+    if (const char* v = getenv("DQDK_GPU_PIECE_SHIFT"))
+        return std::min<uint64_t>((uint64_t)atoll(v) * 256u, kPieceShiftMax - 256u) & ~63ull;
+    return q->piece_shift;
+}
+
 uint32_t* records_part1(const dqdk_gpu_queue* q)
 {
     return q->part1_elems >= q->nk_max + kStagePad ? q->d_part1 : q->d_part1_rec;
@@ -449,7 +462,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     const bool fused = fg != nullptr;
     if (partitioned && (q->hist_pending >= q->hist_k || !q->d_part2))
         return fail_errno(-EIO, "histogram: staging slot out of range");
-    ha.part1 = fused ? q->d_part1 : records_part1(q);
+    ha.part1 = fused ? q->d_part1 + piece_shift(q) : records_part1(q);
     ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
     ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
     if (fused) {
@@ -572,7 +585,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (fused) {
         ra.keys = nullptr;  // no frame-order records
         ra.scratch = slot_scratch;
-        ra.part1 = q->d_part1;
+        ra.part1 = q->d_part1 + piece_shift(q);
         ra.piece_cap = fg.cap;
         ra.piece_words = fg.words;
         ra.region = fg.region;
@@ -1029,12 +1042,14 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                                  ? (uint64_t)kL1Buckets * fg.region
                                  : 0u;
             if (q->fused_elems) {
-                q->part1_elems = q->fused_elems + q->ovf_blk_elems + kStagePad;
+                q->part1_elems = kPieceShiftMax + q->fused_elems + q->ovf_blk_elems + kStagePad;
                 if ((e = dev_alloc(&q->d_part1, q->part1_elems * 4, q->alloc_kind)) != hipSuccess ||
                     (e = hipMalloc(&q->d_ovf, q->ovf_blk_elems * sizeof(uint32_t))) != hipSuccess ||
                     (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                     return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
-                q->d_ovf_blk = q->d_part1 + q->fused_elems;
+                // (the overflow regions sit past every shifted piece region; rx_part1's
+                // output, written once they are dead, may overlap them)
+                q->d_ovf_blk = q->d_part1 + kPieceShiftMax + q->fused_elems;
             }
             if (cfg->flags & (DQDK_GPU_F_BATCH_ABORT | DQDK_GPU_F_HISTO_UNFUSED)) {
                 if (int rc = ensure_records(q, true, true))  // records path every batch

@@ -72,7 +72,28 @@ def main() -> None:
                 q.enable_timing(False)
                 s = q.read_timing()["rx_decode"]
                 times.setdefault(f"q{qi}/{name}", []).append(round(s["ms"] / s["launches"], 4))
-    out = {"frame_len": L, "frames": n, "decode_ms": times,
+    # the same image and queue, the fused pieces moved inside their allocation
+    import os
+    shifts = {}
+    q = queues[0]
+    name, _, t = imgs[0]
+    for rep in range(args.reps):
+        for kib in (0, 64, 256, 1024, 2048, 4096, 8192, 16384):
+            os.environ["DQDK_GPU_PIECE_SHIFT"] = str(kib)
+            for _ in range(2):
+                q.process_device(t.data_ptr(), size, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+            torch.cuda.synchronize(dev)
+            q.read_timing()
+            q.timing_stages(["rx_decode"])
+            q.enable_timing(True)
+            for _ in range(args.steps):
+                q.process_device(t.data_ptr(), size, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+            torch.cuda.synchronize(dev)
+            q.enable_timing(False)
+            s = q.read_timing()["rx_decode"]
+            shifts.setdefault(f"q0/{name}/shift{kib}K", []).append(round(s["ms"] / s["launches"], 4))
+    os.environ.pop("DQDK_GPU_PIECE_SHIFT", None)
+    out = {"frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts,
            "va_mod_2MiB": {name: (t.data_ptr() % (2 << 20)) for name, _, t in imgs}}
     print(json.dumps(out), flush=True)
     for q in queues:
