@@ -93,7 +93,9 @@ def main() -> None:
             s = q.read_timing()["rx_decode"]
             shifts.setdefault(f"q0/{name}/shift{kib}K", []).append(round(s["ms"] / s["launches"], 4))
     os.environ.pop("DQDK_GPU_PIECE_SHIFT", None)
-    out = {"frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts,
+    pr = torch.cuda.get_device_properties(0)
+    out = {"bdf": "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id),
+           "frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts,
            "va_mod_2MiB": {name: (t.data_ptr() % (2 << 20)) for name, _, t in imgs}}
     print(json.dumps(out), flush=True)
     for q in queues:
