@@ -93,9 +93,26 @@ def main() -> None:
             s = q.read_timing()["rx_decode"]
             shifts.setdefault(f"q0/{name}/shift{kib}K", []).append(round(s["ms"] / s["launches"], 4))
     os.environ.pop("DQDK_GPU_PIECE_SHIFT", None)
+    # cheap per-image probes: do they separate the images the decode runs slow on?
+    import ctypes as C
+    from dqdk_amd import _lib as LB
+    ms = C.c_double()
+    fb = (L + 15) // 16 * 16
+    keys = torch.empty(n * ((L - 42) // 16), dtype=torch.int32, device=dev)
+    probes = {}
+    for name, _, t in imgs:
+        LB.check(LB.lib().dqdk_gpu_membench_read(t.data_ptr(), size, stream.cuda_stream, 3, C.byref(ms)), "read")
+        rd = size / (ms.value * 1e-3) / 1e9
+        LB.check(LB.lib().dqdk_gpu_membench_frames(t.data_ptr(), stride, fb, n, None, 0, 0, stream.cuda_stream, 3,
+                                                   C.byref(ms)), "frames")
+        fr = n * fb / (ms.value * 1e-3) / 1e9
+        LB.check(LB.lib().dqdk_gpu_membench_frames(t.data_ptr(), stride, fb, n, keys.data_ptr(), 4 * ((L - 42) // 16), 0,
+                                                   stream.cuda_stream, 3, C.byref(ms)), "frames+w")
+        fw = n * (fb + 4 * ((L - 42) // 16)) / (ms.value * 1e-3) / 1e9
+        probes[name] = {"stream_read_GB_s": round(rd, 1), "frames_read_GB_s": round(fr, 1), "frames_rw_GB_s": round(fw, 1)}
     pr = torch.cuda.get_device_properties(0)
     out = {"bdf": "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id),
-           "frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts,
+           "frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts, "probes": probes,
            "va_mod_2MiB": {name: (t.data_ptr() % (2 << 20)) for name, _, t in imgs}}
     print(json.dumps(out), flush=True)
     for q in queues:
