@@ -109,7 +109,12 @@ def main() -> None:
         LB.check(LB.lib().dqdk_gpu_membench_frames(t.data_ptr(), stride, fb, n, keys.data_ptr(), 4 * ((L - 42) // 16), 0,
                                                    stream.cuda_stream, 3, C.byref(ms)), "frames+w")
         fw = n * (fb + 4 * ((L - 42) // 16)) / (ms.value * 1e-3) / 1e9
-        probes[name] = {"stream_read_GB_s": round(rd, 1), "frames_read_GB_s": round(fr, 1), "frames_rw_GB_s": round(fw, 1)}
+        n4 = min(size // 4096, keys.numel() * 4 // (4 * 91))
+        LB.check(LB.lib().dqdk_gpu_membench_frames(t.data_ptr(), 4096, 1504, n4, keys.data_ptr(), 4 * 91, 0,
+                                                   stream.cuda_stream, 3, C.byref(ms)), "frames4k+w")
+        f4 = n4 * (1504 + 4 * 91) / (ms.value * 1e-3) / 1e9
+        probes[name] = {"stream_read_GB_s": round(rd, 1), "frames_read_GB_s": round(fr, 1), "frames_rw_GB_s": round(fw, 1),
+                        "frames4k_rw_GB_s": round(f4, 1)}
     pr = torch.cuda.get_device_properties(0)
     out = {"bdf": "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id),
            "frame_len": L, "frames": n, "decode_ms": times, "piece_shift_ms": shifts, "probes": probes,
