@@ -163,10 +163,11 @@ void* dqdk_gpu_queue_own_stream(dqdk_gpu_queue_t* q); /* the queue's own one */
 
 /* Device memory for a UMEM image or frame staging slots in HBM (the
  * device-resident and PCIe-inclusive forms).  Physically contiguous when the
- * driver allows (hipDeviceMallocContiguous; else plain device memory): the
- * decode walks frames at their UMEM stride, and from a contiguous image it
- * ran 9000 B batches at 2.27 instead of 2.45 ms per 1M frames on boxes in the
- * fast state (on others every placement decodes alike).
+ * driver allows (hipDeviceMallocContiguous; else plain device memory).  The
+ * 9000 B decode runs 2.12 or 2.35 ms per 1M frames depending on where the
+ * driver placed the image relative to the queue's staging (DESIGN.md
+ * section 5: a placement interaction, not a property of the box); images
+ * from this call ran in the fast state more often than torch's allocator's.
  * Returns 0 (contiguous), 1 (the driver had no contiguous range: plain
  * device memory) or a negative errno.  Allocate large images early:
  * contiguous ranges fragment.  (The queue's own table and staging are plain
