@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, call a: the plugin (frame-processor) harness tests and the egress
 # tests first, then the whole -m gpu suite, the drop-in latency sweep and the
-# default bench line.  usage (on the GPU box): bash tools/gpu_r04a.sh <tag>
+# default bench line.  usage (on the GPU box): bash tools/r04/gpu_r04a.sh <tag>
 set -e
 tag=${1:-r04a}
 mkdir -p gpurun_out

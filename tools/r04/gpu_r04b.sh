@@ -2,7 +2,7 @@
 # Round 4, call b: the new full-size / configs / harness tests first (verbose,
 # with the 8-queue test's latency line), then the rest of the -m gpu suite,
 # the drop-in latency sweep and the default bench line (with box_state).
-# usage (on the GPU box): bash tools/gpu_r04b.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04b.sh <tag>
 set -e
 tag=${1:-r04b}
 mkdir -p gpurun_out

@@ -6,7 +6,7 @@
 #   (W 20 / 16); it_lo = the same at W 16 / 12; nostore = it without piece
 #   stores (timing only); lines = it with whole-line flushes at 1500 B too;
 #   SQ/LDS counters of the default 1500 B and 9000 B runs (one pass each).
-# usage (on the GPU box): bash tools/gpu_r04c.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04c.sh <tag>
 set -e
 tag=${1:-r04c}
 mkdir -p gpurun_out

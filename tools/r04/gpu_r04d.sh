@@ -3,7 +3,7 @@
 # call b (bench rehearsal -> egress -> parity golden), with kernels and copies
 # serialized so an error is reported by the launch that caused it; then the
 # rest of the -m gpu suite, the drop-in latency sweep and the bench line.
-# usage (on the GPU box): bash tools/gpu_r04d.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04d.sh <tag>
 set -e
 tag=${1:-r04d}
 mkdir -p gpurun_out

@@ -5,7 +5,7 @@
 #   round-4 default, folded counters vs rx_abort + rx_count, interleaved frame
 #   map, twice; 9000 B: 5 vs 1, frame maps);
 #   PMC traffic passes of the new default at 1500 B; then every GPU test.
-# usage (on the GPU box): bash tools/gpu_r04i.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04i.sh <tag>
 set -e
 tag=${1:-r04i}
 mkdir -p gpurun_out

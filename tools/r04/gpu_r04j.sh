@@ -3,7 +3,7 @@
 # to the scatter (no LDS round trip; 94 VGPRs, one 16-wave block per CU:
 # build/ab/p2rreg.so) against the working tree (build/ab/base.so), same box,
 # interleaved, both frame sizes; its parity on the partitioned tests first.
-# usage (on the GPU box): bash tools/gpu_r04j.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04j.sh <tag>
 set -e
 tag=${1:-r04j}
 mkdir -p gpurun_out

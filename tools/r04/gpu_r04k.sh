@@ -2,7 +2,7 @@
 # Round 4, call k: the first-line hand-off with the straddling dword carried
 # in a register (policy 6) against the round-4 default (2), folded counters
 # on, same box, twice; its parity tests first; PMC traffic of policy 6.
-# usage (on the GPU box): bash tools/gpu_r04k.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04k.sh <tag>
 set -e
 tag=${1:-r04k}
 mkdir -p gpurun_out

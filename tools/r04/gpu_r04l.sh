@@ -4,7 +4,7 @@
 # default (policy 2) from one build; shnone = the hand-off geometry with
 # phase B reading the straddling dword itself; shload0 = the register dword
 # shifted in but lane 0 loading at the grid offset (wrong bytes: timing only).
-# usage (on the GPU box): bash tools/gpu_r04l.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04l.sh <tag>
 set -e
 tag=${1:-r04l}
 mkdir -p gpurun_out/ab_$tag

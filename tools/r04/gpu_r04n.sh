@@ -3,7 +3,7 @@
 # LDS round trip (cur, policy 6) against policy 2 from the same build, and a
 # timing build whose phase A drops those keys (noastage: where the hand-off's
 # cost sits); same box, interleaved; the hand-off parity tests first.
-# usage (on the GPU box): bash tools/gpu_r04n.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04n.sh <tag>
 set -e
 tag=${1:-r04n}
 mkdir -p gpurun_out/ab_$tag

@@ -2,7 +2,7 @@
 # Round 4, call o: rx_part2's last block re-zeroes the slot's per-batch
 # counters (no memset launch per batch): every GPU test, then A/B on one box
 # against the memset form (DQDK_GPU_P2ZERO=0), 1500 B and 9000 B, twice.
-# usage (on the GPU box): bash tools/gpu_r04o.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04o.sh <tag>
 set -e
 tag=${1:-r04o}
 mkdir -p gpurun_out/ab_$tag

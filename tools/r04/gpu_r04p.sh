@@ -2,7 +2,7 @@
 # Round 4, call p: whole-line flushes at 1500 B with rounds small enough for
 # their carries (fill 46 % -> 12 windows, 40 % -> 8) against the default
 # (triples, 16 windows), same box, twice; plus PMC writes of the best guess.
-# usage (on the GPU box): bash tools/gpu_r04p.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_r04p.sh <tag>
 set -e
 tag=${1:-r04p}
 mkdir -p gpurun_out/ab_$tag

@@ -2,7 +2,7 @@
 # One box's 9000 B speed state and identity: a short 9000 B bench line with
 # box_state (HBM vendor, VBIOS, clocks, partitions) and the decode's
 # fraction of the same-process stream read.
-# usage (on the GPU box): bash tools/gpu_state.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_state.sh <tag>
 set -e
 tag=${1:-state}
 mkdir -p gpurun_out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: the per-process speed state -- tools/state_probe.py in three
 # processes on one box (each: 3 contiguous images + 1 torch image x 2 queues).
-# usage (on the GPU box): bash tools/gpu_state_probe.sh <tag>
+# usage (on the GPU box): bash tools/r04/gpu_state_probe.sh <tag>
 set -e
 tag=${1:-probe}
 mkdir -p gpurun_out
