@@ -383,3 +383,40 @@ def test_raw_stream_synchronous_default_fails_the_same_batch(tmp_path):
     finally:
         q.close()
         os.close(fd)
+
+
+@pytest.mark.parametrize("deferred", [False, True], ids=["sync", "deferred"])
+def test_raw_stream_fused_batches_counter_delta(tmp_path, deferred):
+    """Host drop-in with a raw fd on partitioned energy-histo batches: the
+    fused decode sums the per-packet counters itself (no rx_count), and the
+    call's counter delta, results, raw stream and the table all equal the
+    oracle's, batch by batch."""
+    _need_gpu()
+    cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
+    path = tmp_path / "raw.bin"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    want, okeys_all, ores_all = [], [], []
+    q = D.RxQueue(0, cfg, 4096)
+    try:
+        q.set_raw_fd(fd, deferred=deferred)
+        for b in range(3):
+            umem, desc = D.synth_umem(4096, 1500, 4096, queue=b, faulty=True)
+            ores, ocnt, okeys = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+            res, delta = q.process_batch(umem, desc)
+            np.testing.assert_array_equal(res, ores)
+            for k, v in ocnt.items():
+                assert delta[k] == v, (b, k, delta[k], v)
+            want.append(ref_raw(umem, desc, ores, ocnt, cfg.flags))
+            okeys_all.append(okeys)
+            ores_all.append(ores)
+            q.unregister_umem(umem)
+        q.set_raw_fd(-1)
+        hist = q.histogram()
+    finally:
+        q.close()
+        os.close(fd)
+    assert path.read_bytes() == b"".join(want)
+    u, c = O.sparse_histogram(np.concatenate(okeys_all), np.concatenate(ores_all), cfg.events)
+    nz = np.flatnonzero(hist)
+    np.testing.assert_array_equal(nz.astype(np.uint32), u)
+    np.testing.assert_array_equal(hist[nz].astype(np.uint64), c)
