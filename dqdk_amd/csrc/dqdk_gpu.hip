@@ -182,6 +182,10 @@ struct dqdk_gpu_queue {
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
     uint32_t* d_blkcnt = nullptr;  // fused decode: the folded counters' accumulators (kFoldWords u64)
+#ifdef DQDK_DIAG_TIMING
+    unsigned long long* d_diag = nullptr;
+    bool diag_on = false;
+#endif
     uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
     uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
     uint64_t part1_elems = 0;
@@ -599,6 +603,15 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.hist = q->d_hist;
         // per-packet counters in the decode itself (the host drop-in's
         // publishing batches keep rx_count, which writes its pinned results)
+#ifdef DQDK_DIAG_TIMING  // timing diagnostic builds only: cycle sums printed at destroy
+        if (!q->d_diag)
+            HIPCHK(hipMalloc(&q->d_diag, 4 * sizeof(unsigned long long)));
+        if (!q->diag_on) {
+            HIPCHK(hipMemsetAsync(q->d_diag, 0, 4 * sizeof(unsigned long long), q->stream));
+            q->diag_on = true;
+        }
+        ra.diag = q->d_diag;
+#endif
         ra.fold = !q->publish && !fold_off();
         ra.fmap = frame_map();
         ra.blk_cnt = q->d_blkcnt;
@@ -1146,6 +1159,15 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
         (void)hipStreamSynchronize(q->stream);
     if (q->raw_stream)
         (void)hipStreamSynchronize(q->raw_stream);  // no D2H into h_rawb may outlive it
+#ifdef DQDK_DIAG_TIMING
+    if (q->d_diag) {
+        unsigned long long d[4] = {};
+        if (hipMemcpy(d, q->d_diag, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess && d[2])
+            fprintf(stderr, "diag_timing: waves %llu, phase A %.2f %%, round flushes %.2f %% of the waves' cycles\n",
+                    d[3], 100.0 * d[0] / d[2], 100.0 * d[1] / d[2]);
+        (void)hipFree(q->d_diag);
+    }
+#endif
     for (auto& r : q->regs)
         (void)hipHostUnregister(r.host);
     for (auto& p : q->pending) {

@@ -1420,6 +1420,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     const uint32_t ntiles = (a.n + 63) / 64;
     const uint32_t nsuper = (ntiles + kFWaves - 1) / kFWaves;
     const int W = (int)a.round_windows;
+#ifdef DQDK_DIAG_TIMING
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    uint64_t t_a = 0, t_f = 0;
+#endif
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
         const uint32_t tile = st * kFWaves + wave;
@@ -1430,6 +1434,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         const bool live = i < a.n;
 
         // ---- phase A ----
+#ifdef DQDK_DIAG_TIMING
+        const uint64_t ta0 = __builtin_amdgcn_s_memtime();
+#endif
         FrameInfo fi;
         dqdk_gpu_rx_result_t r;
         LaneFrame lf;
@@ -1455,6 +1462,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             tmax = max(tmax, (int)lds.wtot[w]);
         const int rounds = (tmax + W - 1) / W;  // the same for every wave: the barriers below match
         lds_barrier();                          // wtot is rewritten by the next super-tile
+#ifdef DQDK_DIAG_TIMING
+        t_a += __builtin_amdgcn_s_memtime() - ta0;
+#endif
 
         // ---- phase B: rounds of W windows, the block's stage flushed after each ----
         const uint32_t lane16 = (uint32_t)lane * 16u;
@@ -1559,9 +1569,15 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 #else
             if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
 #endif
+#ifdef DQDK_DIAG_TIMING
+                const uint64_t tf0 = __builtin_amdgcn_s_memtime();
+#endif
                 lds_barrier();
                 fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, false);
                 lds_barrier();
+#ifdef DQDK_DIAG_TIMING
+                t_f += __builtin_amdgcn_s_memtime() - tf0;
+#endif
             }
         }
 
@@ -1608,6 +1624,14 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (tid < kL1Buckets && lds.scnt[tid])
             atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
+#ifdef DQDK_DIAG_TIMING
+    if (lane == 0 && a.diag) {
+        atomicAdd(&a.diag[0], (unsigned long long)t_a);
+        atomicAdd(&a.diag[1], (unsigned long long)t_f);
+        atomicAdd(&a.diag[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+        atomicAdd(&a.diag[3], 1ull);
+    }
+#endif
     if (a.fold)
         fold_publish(a, lds, tid);
 }
