@@ -605,9 +605,9 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         // publishing batches keep rx_count, which writes its pinned results)
 #ifdef DQDK_DIAG_TIMING  // timing diagnostic builds only: cycle sums printed at destroy
         if (!q->d_diag)
-            HIPCHK(hipMalloc(&q->d_diag, 4 * sizeof(unsigned long long)));
+            HIPCHK(hipMalloc(&q->d_diag, 6 * sizeof(unsigned long long)));
         if (!q->diag_on) {
-            HIPCHK(hipMemsetAsync(q->d_diag, 0, 4 * sizeof(unsigned long long), q->stream));
+            HIPCHK(hipMemsetAsync(q->d_diag, 0, 6 * sizeof(unsigned long long), q->stream));
             q->diag_on = true;
         }
         ra.diag = q->d_diag;
@@ -1161,10 +1161,12 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
         (void)hipStreamSynchronize(q->raw_stream);  // no D2H into h_rawb may outlive it
 #ifdef DQDK_DIAG_TIMING
     if (q->d_diag) {
-        unsigned long long d[4] = {};
+        unsigned long long d[6] = {};
         if (hipMemcpy(d, q->d_diag, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess && d[2])
-            fprintf(stderr, "diag_timing: waves %llu, phase A %.2f %%, round flushes %.2f %% of the waves' cycles\n",
-                    d[3], 100.0 * d[0] / d[2], 100.0 * d[1] / d[2]);
+            fprintf(stderr,
+                    "diag_timing: waves %llu, phase A %.2f %%, round flushes %.2f %% (first barrier wait %.2f %%, "
+                    "flush work %.2f %%) of the waves' cycles\n",
+                    d[3], 100.0 * d[0] / d[2], 100.0 * d[1] / d[2], 100.0 * d[4] / d[2], 100.0 * d[5] / d[2]);
         (void)hipFree(q->d_diag);
     }
 #endif

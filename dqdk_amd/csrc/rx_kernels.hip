@@ -1422,7 +1422,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     const int W = (int)a.round_windows;
 #ifdef DQDK_DIAG_TIMING
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
-    uint64_t t_a = 0, t_f = 0;
+    uint64_t t_a = 0, t_f = 0, t_w1 = 0, t_fw = 0;
 #endif
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
@@ -1573,7 +1573,14 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 const uint64_t tf0 = __builtin_amdgcn_s_memtime();
 #endif
                 lds_barrier();
+#ifdef DQDK_DIAG_TIMING
+                const uint64_t tf1 = __builtin_amdgcn_s_memtime();
+                t_w1 += tf1 - tf0;
+#endif
                 fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, false);
+#ifdef DQDK_DIAG_TIMING
+                t_fw += __builtin_amdgcn_s_memtime() - tf1;
+#endif
                 lds_barrier();
 #ifdef DQDK_DIAG_TIMING
                 t_f += __builtin_amdgcn_s_memtime() - tf0;
@@ -1630,6 +1637,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         atomicAdd(&a.diag[1], (unsigned long long)t_f);
         atomicAdd(&a.diag[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
         atomicAdd(&a.diag[3], 1ull);
+        atomicAdd(&a.diag[4], (unsigned long long)t_w1);
+        atomicAdd(&a.diag[5], (unsigned long long)t_fw);
     }
 #endif
     if (a.fold)
