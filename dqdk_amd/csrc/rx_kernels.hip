@@ -1119,31 +1119,68 @@ __device__ __forceinline__ void ovf_put(const RxArgs& a, __amdgpu_buffer_rsrc_t 
         __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Each bucket's stage is a ring of kFCap slots: its counter scnt[b] packs the
-// ring's head (low 8 bits) and the staged keys (high 24 bits: a round adds
-// at most 64 x 16 x 128 keys to one bucket), so one returning add of
-// kCntUnit gives a key both its ring slot and the capacity check, and a
-// flush only advances the head past what it wrote -- the keys it leaves (a
-// partial triple or line) stay where they are, no carry is copied.
-// (Per-frame out-of-bounds counts and the lanes' sink words step by the same
-// unit: their counts are value >> 8.)
-constexpr uint32_t kCntShift = 8;
-constexpr uint32_t kCntUnit = 1u << kCntShift;
-static_assert(kFCap < (int)kCntUnit, "ring head must fit below the count");
-__device__ __forceinline__ uint32_t ring_slot(uint32_t v)  // counter value -> ring slot of the next key
+// One event per 16-B chunk (as decode_chunk): the key goes to the LDS stage
+// of its bucket; past kFCap staged keys (rare) it goes to the block's private
+// overflow region.  The overflow store is issued by every lane of every
+// window (dropped out of range unless the key overflows) and its slot comes
+// from an LDS counter: the window loop's VMEM pattern stays fixed, so the
+// compiler waits for ring loads with vmcnt(N) instead of draining the ring (a
+// conditional global atomic or store here would force near-full waits).
+__device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef,
+                                            uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc)
 {
-    const uint32_t p = (v & (kCntUnit - 1)) + (v >> kCntShift);
-    return p >= (uint32_t)kFCap ? p - (uint32_t)kFCap : p;
+    const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
+    const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
+    const uint32_t ch = x & 0xffffu;
+    const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
+    const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
+    const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
+    const bool inb = ch < kChannels && hc < kHists;                  // histogram_event's bounds (tristan.c:236-241)
+    // one returning LDS add per event, to the bucket's stage count or to the
+    // frame's out-of-bounds count, and one masked stage store: two masked
+    // operations instead of two levels of divergent branches (decode -2 % at
+    // 1500 B, A/B on one box; the same at 9000 B)
+    const bool has = e < Ef;
+    const uint32_t b = key >> kL1Shift;
+    uint32_t* const cnt = inb ? &lds.scnt[min(b, (uint32_t)kL1Buckets - 1)] : &lds.oob[oob_slot];
+    uint32_t slot = 0;
+    if (has)
+        slot = atomicAdd(cnt, 1u);
+    const bool ink = has && inb;
+    if (ink && slot < (uint32_t)kFCap)
+        lds.stage[b * kFCap + slot] = key;
+    const bool ov = ink && slot >= (uint32_t)kFCap;
+
+    // overflow slots: one LDS atomic per wave (lanes ranked by mbcnt), not one
+    // per key on the block's single counter (64 lanes on one address serialise)
+    const uint64_t om = __ballot(ov);
+    if (om) {
+        const uint32_t first = (uint32_t)__builtin_ctzll(om);
+        uint32_t base = 0;
+        if ((uint32_t)(threadIdx.x & 63) == first)
+            base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
+        base = rdl(base, first);
+        ovf_put(a, ovf_rsrc, key, ov,
+                base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, kOOB, 0, 0);
+    }
 }
 
 // Both chunks of a window at once, without divergent branches: every lane
 // issues two returning LDS adds (an event's bucket stage count, a frame's
 // out-of-bounds count, or -- lanes without an event -- a private sink word of
-// the lane), one wait, then two stage stores (a full ring, or no event: the
-// lane's sink word).  The stage counts' latency is paid once per window
+// the lane), one wait, then two stage stores (a slot past kFCap, or no event:
+// the lane's sink word).  The stage counts' latency is paid once per window
 // instead of once per chunk, and no exec mask is saved or restored.  Keys
 // past kFCap (rare) go to the block's overflow region behind one
 // wave-uniform branch.
+#ifndef DQDK_FPAIR
+#define DQDK_FPAIR 1
+#endif
+// Stage counts (and per-frame out-of-bounds counts) step by kCntUnit: with 4
+// a count is the byte offset of the slot, so a stage address is one mad.
+constexpr uint32_t kCntUnit = DQDK_FPAIR >= 2 ? 4u : 1u;
 __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0,
                                            uint32_t Ef, uint32_t oob_slot, FusedLds& lds,
                                            __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane)
@@ -1151,8 +1188,8 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     uint32_t key[2], b[2];
     uint32_t* cnt[2];
     bool ink[2];
-    // the lane's sink: the 64 slack words after the last bucket's ring (never
-    // read by a flush: ring indices stay inside their bucket)
+    // the lane's sink: the 64 slack words after the last bucket's stage (read
+    // by the flush of bucket 283 only past its count, so never stored)
     uint32_t* const sink = &lds.stage[kL1Buckets * kFCap + lane];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
@@ -1169,14 +1206,27 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
         ink[c] = has && inb;
         cnt[c] = has ? (inb ? &lds.scnt[b[c]] : &lds.oob[oob_slot]) : sink;
     }
+#if DQDK_FPAIR >= 2
+    // counts in bytes: the slot's stage address is b * (4 kFCap) + count
     const uint32_t s0 = atomicAdd(cnt[0], kCntUnit);
     const uint32_t s1 = atomicAdd(cnt[1], kCntUnit);
-    const bool st0 = ink[0] && (s0 >> kCntShift) < (uint32_t)kFCap, st1 = ink[1] && (s1 >> kCntShift) < (uint32_t)kFCap;
-    *(st0 ? &lds.stage[b[0] * kFCap + ring_slot(s0)] : sink) = key[0];
-    *(st1 ? &lds.stage[b[1] * kFCap + ring_slot(s1)] : sink) = key[1];
-    const bool ov0 = ink[0] && !st0, ov1 = ink[1] && !st1;
+    const bool st0 = ink[0] && s0 < 4u * kFCap, st1 = ink[1] && s1 < 4u * kFCap;
+    uint8_t* const stage8 = (uint8_t*)lds.stage;
+    *(uint32_t*)(st0 ? stage8 + __umul24(b[0], 4u * kFCap) + s0 : (uint8_t*)sink) = key[0];
+    *(uint32_t*)(st1 ? stage8 + __umul24(b[1], 4u * kFCap) + s1 : (uint8_t*)sink) = key[1];
+    const bool ov0 = ink[0] && s0 >= 4u * kFCap, ov1 = ink[1] && s1 >= 4u * kFCap;
+    if (__builtin_amdgcn_ballot_w64(ov0 || ov1)) {  // rare: overflow slots, one LDS atomic per wave
+        const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
+#else
+    const uint32_t s0 = atomicAdd(cnt[0], 1u);
+    const uint32_t s1 = atomicAdd(cnt[1], 1u);
+    const bool st0 = ink[0] && s0 < (uint32_t)kFCap, st1 = ink[1] && s1 < (uint32_t)kFCap;
+    *(st0 ? &lds.stage[b[0] * kFCap + s0] : sink) = key[0];
+    *(st1 ? &lds.stage[b[1] * kFCap + s1] : sink) = key[1];
+    const bool ov0 = ink[0] && s0 >= (uint32_t)kFCap, ov1 = ink[1] && s1 >= (uint32_t)kFCap;
     const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
     if (m0 | m1) {  // rare: overflow slots, one LDS atomic per wave
+#endif
         const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
         const uint32_t first = (uint32_t)__builtin_ctzll(m0 | m1);
         uint32_t base = 0;
@@ -1211,14 +1261,14 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
     for (int k = 0; k < kAEv; k++) {
         const bool ink = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE;
         const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
-        const bool st = ink && (sl[k] >> kCntShift) < (uint32_t)kFCap;
-        *(st ? &lds.stage[b * kFCap + ring_slot(sl[k])] : sink) = akey[k];
+        const bool st = ink && sl[k] < kCntUnit * kFCap;
+        *(st ? &lds.stage[b * kFCap + sl[k] / kCntUnit] : sink) = akey[k];
         anyov |= ink && !st;
     }
     if (__ballot(anyov)) {  // rare: overflow slots
 #pragma unroll
         for (int k = 0; k < kAEv; k++) {
-            const bool ov = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE && (sl[k] >> kCntShift) >= (uint32_t)kFCap;
+            const bool ov = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE && sl[k] >= kCntUnit * kFCap;
             const uint64_t om = __ballot(ov);
             if (om) {
                 const uint32_t first = (uint32_t)__builtin_ctzll(om);
@@ -1249,11 +1299,9 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
                                             __amdgpu_buffer_rsrc_t ovf_rsrc, bool last)
 {
     const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
-    uint32_t c = 0, w = 0, fit = 0, head = 0;
+    uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
-        const uint32_t sv = lds.scnt[b];
-        head = sv & (kCntUnit - 1);
-        c = min(sv >> kCntShift, (uint32_t)kFCap);
+        c = min(lds.scnt[b] / kCntUnit, (uint32_t)kFCap);
         // lines policy: whole 128-B lines of triples (the piece cursor stays
         // line-aligned, so no store writes part of a line); else whole triples
 #ifndef DQDK_FLUSH_UNIT
@@ -1276,13 +1324,9 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
 #pragma unroll
         for (int q = 0; q < G; q++) {
             const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(h * G + q), (uint32_t)kL1Buckets - 1);
-            const uint32_t hj = rdl(head, min(h * G + q, 63));  // the bucket's ring head
 #pragma unroll
-            for (int i = 0; i < 3; i++) {  // (lanes past the run read another slot of the ring: unused)
-                uint32_t x = hj + 3u * (uint32_t)lane + (uint32_t)i;
-                x = x >= (uint32_t)kFCap ? x - (uint32_t)kFCap : x;
-                v[q][i] = lds.stage[bj * kFCap + min(x, (uint32_t)kFCap - 1)];
-            }
+            for (int i = 0; i < 3; i++)  // (lanes past the run read the next bucket's stage or the sink: unused)
+                v[q][i] = lds.stage[bj * kFCap + 3 * lane + i];
         }
 #pragma unroll
         for (int q = 0; q < G; q++) {
@@ -1314,20 +1358,30 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
         if (lane == 0)
             o = atomicAdd(&lds.ovf_n, nov);
         o = rfl(o);
-        const uint32_t hj = rdl(head, j);
-        for (uint32_t t = (uint32_t)lane; t < nov; t += 64) {
-            uint32_t x = hj + fj + t;  // (< 2 kFCap)
-            x = x >= (uint32_t)kFCap ? x - (uint32_t)kFCap : x;
-            ovf_put(a, ovf_rsrc, lds.stage[bj * kFCap + x], true, o + t);
+        for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
+            ovf_put(a, ovf_rsrc, lds.stage[bj * kFCap + fj + t], true, o + t);
+    }
+    // carry the remainders to the stage's start (fewer keys than were
+    // flushed, so source and destination do not overlap)
+    if (kLines) {  // up to 47 keys: a wave per bucket
+        for (uint64_t m = __ballot(w != 0 && c > w); m; m &= m - 1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            const uint32_t bj = wave + (uint32_t)kFWaves * j;
+            const uint32_t wj = rdl(w, j), r = rdl(c, j) - wj;
+            uint32_t x = 0;
+            if ((uint32_t)lane < r)
+                x = lds.stage[bj * kFCap + wj + lane];
+            if ((uint32_t)lane < r)
+                lds.stage[bj * kFCap + lane] = x;
         }
+    } else if (w != 0 && c > w) {  // up to 2 keys: each lane its own bucket
+        const uint32_t x0 = lds.stage[b * kFCap + w], x1 = lds.stage[b * kFCap + w + 1];
+        lds.stage[b * kFCap] = x0;
+        if (c - w > 1)
+            lds.stage[b * kFCap + 1] = x1;
     }
-    // the keys left (a partial triple or line) stay in the ring: its head
-    // moves past the flushed ones (the last flush leaves every counter 0)
-    if (b < (uint32_t)kL1Buckets) {
-        uint32_t nh = head + w;
-        nh = nh >= (uint32_t)kFCap ? nh - (uint32_t)kFCap : nh;
-        lds.scnt[b] = last ? 0u : (nh | ((c - w) << kCntShift));
-    }
+    if (b < (uint32_t)kL1Buckets)
+        lds.scnt[b] = (c - w) * kCntUnit;
 }
 
 // Two policies for the pieces' partial lines (runs end mid-line), chosen by
@@ -1491,7 +1545,12 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
+#if DQDK_FPAIR
                 fused_pair(a, b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
+#else
+                fused_chunk(a, b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
+                fused_chunk(a, b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
+#endif
                 if (active && ++wp == P.nwin) {
                     frame_sum_add(&lds.sum[wslot0 + jp], &lds.stage[kL1Buckets * kFCap + lane], acc0 + acc1,
                                   (lane & 15) == 15);
@@ -1531,7 +1590,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 
         // ---- phase C ----
         const uint32_t my = wslot0 + (uint32_t)lane;
-        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my] >> kCntShift;
+        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my] / kCntUnit;
         lds.sum[my] = 0;
         lds.oob[my] = 0;
 #if DQDK_INLINE_TAIL
