@@ -182,14 +182,10 @@ struct dqdk_gpu_queue {
     dqdk_gpu_counters_t* d_cum = nullptr;
     uint64_t* d_batch = nullptr;
     uint32_t* d_blkcnt = nullptr;  // fused decode: the folded counters' accumulators (kFoldWords u64)
-#ifdef DQDK_DIAG_TIMING
-    unsigned long long* d_diag = nullptr;
-    bool diag_on = false;
-#endif
     uint32_t* d_keys = nullptr;    // records path: frame-order keys (max_batch * E; allocated on first use)
     uint32_t* d_part1 = nullptr;   // fused path: pieces + rx_part1's copy of the overflow list (part1_elems)
     uint64_t part1_elems = 0;
-    uint64_t piece_shift = 0;      // fused pieces start this many words into d_part1 (< kPieceShiftMax)
+    uint64_t piece_shift = 0;      // fused pieces start this many words into d_part1 (DQDK_GPU_PIECE_SHIFT)
     uint32_t* d_part1_rec = nullptr;  // records path: rx_part1's output when d_part1 is smaller (first use)
     uint32_t* d_ovf = nullptr;     // fused path: the overflow list (ovf_blk_elems keys)
     uint32_t ovf_cap_blk = 0;      // fused path: keys per block overflow region
@@ -207,6 +203,14 @@ struct dqdk_gpu_queue {
     uint64_t nk_max = 0;           // max_batch * E
     uint64_t scratch_words = 0;    // kHistScratchWords per staged slot
     int histo_path = 0;            // 0 auto, 1 atomic, 2 partitioned
+    // A/B knobs (DQDK_GPU_* environment), read once by dqdk_gpu_queue_create
+    // and never per batch: the engine's behaviour is fixed for the queue's life
+    uint32_t fused_pol = 0;        // fused decode variant (fused_policy)
+    uint32_t round_windows = 0;    // fused decode windows per wave per round (fused_round_windows)
+    bool fold_off = false;         // DQDK_GPU_FOLD=0: the fused path counts in rx_abort + rx_count launches
+    uint32_t fmap = 0;             // DQDK_GPU_FRAME_MAP=1: interleaved fused frame map
+    bool p2zero_off = false;       // DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch
+    bool small_off = false;        // DQDK_GPU_SMALL=0: small batches take the three-launch form too
     int alloc_kind = 0;            // device memory of the table and staging (dev_alloc)
     // Partitioned batches stage their slice-sorted keys (part2 + runs +
     // scratch, one slot each); the slice pass -- which sweeps the low-byte
@@ -360,26 +364,24 @@ int hist_flush(dqdk_gpu_queue* q)
 // phase A takes each frame's first line (events and checksum bytes; phase B
 // then never touches that line: traffic 2.08 -> 1.96 GB at 1M x 1500 B, but
 // the decode 0.432 -> 0.455 ms on one box, r04k2: the extra phase-A work
-// costs more than the line, so it is off by default).  DQDK_GPU_FUSED_POLICY
-// =<0..7> overrides it per batch (A/B on one box; the tests run every variant).
+// costs more than the line, so it is off by default).  The shipped library
+// holds the two default variants (1 from 128 events per frame, else 2);
+// a build with -DDQDK_AB_VARIANTS holds all eight, which
+// DQDK_GPU_FUSED_POLICY=<0..7> selects at queue creation (A/B, tests).
 #ifndef DQDK_FUSED_POLICY
 #define DQDK_FUSED_POLICY (E >= 128 ? 1u : 2u)
 #endif
-uint32_t fused_policy(uint32_t E)
-{
-    const char* s = getenv("DQDK_GPU_FUSED_POLICY");
-    return s && *s ? (uint32_t)atoi(s) & 7u : (uint32_t)(DQDK_FUSED_POLICY);
-}
+uint32_t fused_policy_default(uint32_t E) { return (uint32_t)(DQDK_FUSED_POLICY); }
 
-uint32_t fused_round_windows(uint32_t E)
+#ifdef DQDK_AB_VARIANTS
+constexpr uint32_t kFusedPolicies = 0xffu;  // every variant built
+#else
+constexpr uint32_t kFusedPolicies = (1u << 1) | (1u << 2);
+#endif
+
+uint32_t fused_round_windows(uint32_t E, double fill)
 {
     const uint32_t epw = std::max<uint32_t>(1, std::min<uint32_t>(E, 128));
-#ifndef DQDK_FUSED_FILL  // (134-key stage: W = 16 at 1500 B, 12 at 9000 B; A/B r04g: 20 / 16 slower)
-#define DQDK_FUSED_FILL (E >= 128 ? 65 : 61)
-#endif
-    double fill = DQDK_FUSED_FILL;
-    if (const char* v = getenv("DQDK_GPU_FUSED_FILL"))  // (A/B only: stage fill target in percent)
-        fill = atof(v);
     const uint32_t w = (uint32_t)(fill / 100.0 * kFCap * kL1Buckets / (kFWaves * epw));
     const uint32_t wr = (w + kFRingW / 2) / kFRingW * kFRingW;  // nearest multiple of the ring depth
     return std::max<uint32_t>(kFRingW, std::min<uint32_t>(64, wr));
@@ -403,15 +405,6 @@ int ensure_records(dqdk_gpu_queue* q, bool keys, bool part1)
         return (fail("hipMalloc(records)", e), -ENOMEM);
     }
     return 0;
-}
-
-// The fused pieces' offset in words; DQDK_GPU_PIECE_SHIFT (KiB) overrides it
-// per batch (A/B and tools/state_probe.py)
-uint64_t piece_shift(const dqdk_gpu_queue* q)
-{
-    if (const char* v = getenv("DQDK_GPU_PIECE_SHIFT"))
-        return std::min<uint64_t>((uint64_t)atoll(v) * 256u, kPieceShiftMax - 256u) & ~63ull;
-    return q->piece_shift;
 }
 
 uint32_t* records_part1(const dqdk_gpu_queue* q)
@@ -466,7 +459,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     const bool fused = fg != nullptr;
     if (partitioned && (q->hist_pending >= q->hist_k || !q->d_part2))
         return fail_errno(-EIO, "histogram: staging slot out of range");
-    ha.part1 = fused ? q->d_part1 + piece_shift(q) : records_part1(q);
+    ha.part1 = fused ? q->d_part1 + q->piece_shift : records_part1(q);
     ha.part2 = q->d_part2 ? q->d_part2 + q->hist_pending * q->part2_stride : nullptr;
     ha.runs = q->d_runs ? q->d_runs + q->hist_pending * q->runs_stride : nullptr;
     if (fused) {
@@ -504,7 +497,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     {
         StageTimer t(q, kStPart2);
         // non-temporal key loads where the fused decode's are (fused_policy bit 1)
-        if (fused_policy(q->E) & 2u)
+        if (q->fused_pol & 2u)
             hipLaunchKernelGGL(rx_part2_kernel<2>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
         else
             hipLaunchKernelGGL(rx_part2_kernel<0>, dim3(grid_l2), dim3(kPartThreads), 0, q->stream, ha);
@@ -517,11 +510,6 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     return 0;
 }
 
-bool small_off();
-bool fold_off();
-uint32_t frame_map();
-bool part2_zero_off();
-
 // The staged slot's per-batch counters are zero before its batch's first
 // kernel: a memset only when the slot's last rx_part2 did not re-zero them
 // (first use, or a batch that failed on the way); dirty until this batch's
@@ -530,9 +518,60 @@ int clean_slot(dqdk_gpu_queue* q, uint32_t* slot_scratch)
 {
     if (q->slot_dirty.size() < q->hist_k)
         q->slot_dirty.resize(q->hist_k, 1);
-    if (q->slot_dirty[q->hist_pending] || part2_zero_off())
+    if (q->slot_dirty[q->hist_pending] || q->p2zero_off)
         HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
     q->slot_dirty[q->hist_pending] = 1;
+    return 0;
+}
+
+// The fused decode variant of a policy (fused_policy_default; the variants
+// kFusedPolicies does not hold are not in this build's code object).
+void (*fused_kernel(uint32_t pol))(RxArgs)
+{
+    switch (pol) {
+    case 1: return rx_decode_fused_kernel<0, true, false>;
+    case 2: return rx_decode_fused_kernel<2, false, false>;
+#ifdef DQDK_AB_VARIANTS
+    case 0: return rx_decode_fused_kernel<0, false, false>;
+    case 3: return rx_decode_fused_kernel<2, true, false>;
+    case 4: return rx_decode_fused_kernel<0, false, true>;
+    case 5: return rx_decode_fused_kernel<0, true, true>;
+    case 6: return rx_decode_fused_kernel<2, false, true>;
+    case 7: return rx_decode_fused_kernel<2, true, true>;
+#endif
+    default: return nullptr;
+    }
+}
+
+// The A/B knobs, once per queue (dqdk_gpu_queue_create).  Returns -EINVAL for
+// a fused policy this build does not hold.
+int read_knobs(dqdk_gpu_queue* q)
+{
+    auto env = [](const char* k) -> const char* {
+        const char* v = getenv(k);
+        return v && *v ? v : nullptr;
+    };
+    q->fused_pol = fused_policy_default(q->E);
+    if (const char* v = env("DQDK_GPU_FUSED_POLICY")) {
+        const uint32_t p = (uint32_t)atoi(v) & 7u;
+        if (!((kFusedPolicies >> p) & 1u))
+            return fail_errno(-EINVAL, ("queue_create: DQDK_GPU_FUSED_POLICY=" + std::to_string(p) +
+                                        " is an A/B variant (build with -DDQDK_AB_VARIANTS)").c_str());
+        q->fused_pol = p;
+    }
+#ifndef DQDK_FUSED_FILL  // stage fill target, percent (134-key stage: W = 16 at 1500 B, 12 at 9000 B; r04g: 20 / 16 slower)
+#define DQDK_FUSED_FILL (q->E >= 128 ? 65 : 61)
+#endif
+    double fill = DQDK_FUSED_FILL;
+    if (const char* v = env("DQDK_GPU_FUSED_FILL"))
+        fill = atof(v);
+    q->round_windows = fused_round_windows(q->E, fill);
+    q->fold_off = env("DQDK_GPU_FOLD") && !strcmp(env("DQDK_GPU_FOLD"), "0");
+    q->fmap = env("DQDK_GPU_FRAME_MAP") ? (uint32_t)(atoi(env("DQDK_GPU_FRAME_MAP")) != 0) : 0u;
+    q->p2zero_off = env("DQDK_GPU_P2ZERO") && !strcmp(env("DQDK_GPU_P2ZERO"), "0");
+    q->small_off = env("DQDK_GPU_SMALL") && !strcmp(env("DQDK_GPU_SMALL"), "0");
+    if (const char* v = env("DQDK_GPU_PIECE_SHIFT"))  // KiB (tools/state_probe.py)
+        q->piece_shift = std::min<uint64_t>((uint64_t)atoll(v) * 256u, kPieceShiftMax - 256u) & ~63ull;
     return 0;
 }
 
@@ -589,13 +628,13 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (fused) {
         ra.keys = nullptr;  // no frame-order records
         ra.scratch = slot_scratch;
-        ra.part1 = q->d_part1 + piece_shift(q);
+        ra.part1 = q->d_part1 + q->piece_shift;
         ra.piece_cap = fg.cap;
         ra.piece_words = fg.words;
         ra.region = fg.region;
         ra.ovf = q->d_ovf;
         ra.fix = q->d_fix;
-        ra.round_windows = fused_round_windows(q->E);
+        ra.round_windows = q->round_windows;
         const uint32_t grid = fg.grid;
         // private overflow regions of ovf_cap_blk keys (past them: the table)
         ra.ovf_blk = q->d_ovf_blk;
@@ -603,17 +642,8 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.hist = q->d_hist;
         // per-packet counters in the decode itself (the host drop-in's
         // publishing batches keep rx_count, which writes its pinned results)
-#ifdef DQDK_DIAG_TIMING  // timing diagnostic builds only: cycle sums printed at destroy
-        if (!q->d_diag)
-            HIPCHK(hipMalloc(&q->d_diag, 6 * sizeof(unsigned long long)));
-        if (!q->diag_on) {
-            HIPCHK(hipMemsetAsync(q->d_diag, 0, 6 * sizeof(unsigned long long), q->stream));
-            q->diag_on = true;
-        }
-        ra.diag = q->d_diag;
-#endif
-        ra.fold = !q->publish && !fold_off();
-        ra.fmap = frame_map();
+        ra.fold = !q->publish && !q->fold_off;
+        ra.fmap = q->fmap;
         ra.blk_cnt = q->d_blkcnt;
         ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
         ra.cum = q->d_cum;
@@ -621,15 +651,11 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
             return fail_errno(-EINVAL, "fused decode: overflow regions exceed their allocation");
         StageTimer t(q, kStDecode);
         // partial-line policy by frame density (fused_policy)
-        const uint32_t pol = fused_policy(q->E);
-        static void (*const kFused[8])(RxArgs) = {
-            rx_decode_fused_kernel<0, false, false>, rx_decode_fused_kernel<0, true, false>,
-            rx_decode_fused_kernel<2, false, false>, rx_decode_fused_kernel<2, true, false>,
-            rx_decode_fused_kernel<0, false, true>,  rx_decode_fused_kernel<0, true, true>,
-            rx_decode_fused_kernel<2, false, true>,  rx_decode_fused_kernel<2, true, true>};
-        auto kern = kFused[pol & 7u];
+        auto kern = fused_kernel(q->fused_pol);
+        if (!kern)
+            return fail_errno(-EINVAL, "fused decode: no such variant");
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
-    } else if (n <= (uint32_t)kTile && !small_off()) {
+    } else if (n <= (uint32_t)kTile && !q->small_off) {
         // one block: decode, abort and count in a single launch (rx_small),
         // the frames spread over all its waves (a 64-frame batch is four
         // 16-frame tiles, not one wave streaming 64 frames in a row: over
@@ -648,7 +674,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     HIPCHK(hipGetLastError());
 
-    if (fused ? !ra.fold : (n > (uint32_t)kTile || small_off())) {
+    if (fused ? !ra.fold : (n > (uint32_t)kTile || q->small_off)) {
         const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
         {
             StageTimer t(q, kStAbort);
@@ -670,42 +696,6 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     if (q->histo && q->E)
         return launch_histo(q, n, d_res, keys, partitioned, fused ? &fg : nullptr, ra, slot_scratch);
     return 0;
-}
-
-// DQDK_GPU_FOLD=0: the fused path counts in rx_abort + rx_count launches (A/B only)
-bool fold_off()
-{
-    const char* v = getenv("DQDK_GPU_FOLD");
-    return v && !strcmp(v, "0");
-}
-
-// The fused decode's frame map: 0 = each wave streams 64 consecutive
-// frames, 1 = a block's waves stream 16 adjacent frames at a time
-// (DQDK_GPU_FRAME_MAP overrides per batch)
-#ifndef DQDK_FRAME_MAP
-#define DQDK_FRAME_MAP 0u
-#endif
-uint32_t frame_map()
-{
-    const char* v = getenv("DQDK_GPU_FRAME_MAP");
-    return v && *v ? (uint32_t)(atoi(v) != 0) : (uint32_t)(DQDK_FRAME_MAP);
-}
-
-// DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch (A/B only)
-bool part2_zero_off()
-{
-    const char* v = getenv("DQDK_GPU_P2ZERO");
-    return v && !strcmp(v, "0");
-}
-
-// DQDK_GPU_SMALL=0: small batches take the three-launch form too (A/B only)
-bool small_off()
-{
-    static const bool off = [] {
-        const char* v = getenv("DQDK_GPU_SMALL");
-        return v && !strcmp(v, "0");
-    }();
-    return off;
 }
 
 // The frame-processor plugin's batch (frame_processor.hip): n staged
@@ -988,6 +978,10 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
     if (const char* v = getenv("DQDK_GPU_DECODE_CUS"))
         q->dec_cus = std::max(1, std::min(q->cu_count, atoi(v)));
     q->alloc_kind = internal_alloc_kind(q->E);
+    if (int rc = read_knobs(q)) {
+        delete q;
+        return rc;
+    }
     if (cfg->flags & DQDK_GPU_F_HISTO_ATOMIC)
         q->histo_path = 1;
     else if (cfg->flags & DQDK_GPU_F_HISTO_PARTITIONED)
@@ -1055,14 +1049,14 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                                  ? (uint64_t)kL1Buckets * fg.region
                                  : 0u;
             if (q->fused_elems) {
-                q->part1_elems = kPieceShiftMax + q->fused_elems + q->ovf_blk_elems + kStagePad;
+                q->part1_elems = q->piece_shift + q->fused_elems + q->ovf_blk_elems + kStagePad;
                 if ((e = dev_alloc(&q->d_part1, q->part1_elems * 4, q->alloc_kind)) != hipSuccess ||
                     (e = hipMalloc(&q->d_ovf, q->ovf_blk_elems * sizeof(uint32_t))) != hipSuccess ||
                     (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
                     return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
                 // (the overflow regions sit past every shifted piece region; rx_part1's
                 // output, written once they are dead, may overlap them)
-                q->d_ovf_blk = q->d_part1 + kPieceShiftMax + q->fused_elems;
+                q->d_ovf_blk = q->d_part1 + q->piece_shift + q->fused_elems;
             }
             if (cfg->flags & (DQDK_GPU_F_BATCH_ABORT | DQDK_GPU_F_HISTO_UNFUSED)) {
                 if (int rc = ensure_records(q, true, true))  // records path every batch
@@ -1159,17 +1153,6 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
         (void)hipStreamSynchronize(q->stream);
     if (q->raw_stream)
         (void)hipStreamSynchronize(q->raw_stream);  // no D2H into h_rawb may outlive it
-#ifdef DQDK_DIAG_TIMING
-    if (q->d_diag) {
-        unsigned long long d[6] = {};
-        if (hipMemcpy(d, q->d_diag, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess && d[2])
-            fprintf(stderr,
-                    "diag_timing: waves %llu, phase A %.2f %%, round flushes %.2f %% (first barrier wait %.2f %%, "
-                    "flush work %.2f %%) of the waves' cycles\n",
-                    d[3], 100.0 * d[0] / d[2], 100.0 * d[1] / d[2], 100.0 * d[4] / d[2], 100.0 * d[5] / d[2]);
-        (void)hipFree(q->d_diag);
-    }
-#endif
     for (auto& r : q->regs)
         (void)hipHostUnregister(r.host);
     for (auto& p : q->pending) {

@@ -194,9 +194,6 @@ struct RxArgs {
     uint32_t* blk_cnt;
     uint32_t* ticket;         // zero between launches
     dqdk_gpu_counters_t* cum;
-#ifdef DQDK_DIAG_TIMING  // timing diagnostic builds only: per-wave cycle sums (phase A, flushes, whole)
-    unsigned long long* diag;
-#endif
 };
 constexpr int kFoldWords = 16;
 

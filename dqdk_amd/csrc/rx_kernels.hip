@@ -181,11 +181,7 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         u32x4 v = {0u, 0u, 0u, 0u};
-#ifdef DQDK_DIAG_NOHDR  // timing diagnostic only: every lane parses frame 0's header line
-        uint64_t o = (a.desc[0].addr & ~15ull) + 16ull * k;
-#else
         uint64_t o = a0 + 16ull * k;
-#endif
         if (addr < a.umem_size && o + 16 <= a.umem_size)
             v = *(const u32x4*)(a.umem + o);
         w[4 * k + 0] = v.x;
@@ -454,6 +450,14 @@ __device__ __forceinline__ bool udp_csum_ok(uint32_t S, uint32_t check, uint32_t
 constexpr uint32_t kOOB = 0x80000000u;  // buffer offset beyond every SRD's num_records
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+// a VGPR value the compiler cannot see through: per-lane addresses derived
+// from it are recomputed where used instead of hoisted out of a loop (live
+// across it, they spill)
+__device__ __forceinline__ uint32_t opaque(uint32_t v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
@@ -699,9 +703,6 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
                  ((fi.work & 1u) << 22) | ((lw ? 1u : 0u) << 23) | (((ct >> 6) & 1u) << 24) | ((ct & 63u) << 25);
         const uint32_t tw = tc ? ct / (uint32_t)kWinChunks : kNoWin;
         const uint32_t mw = lw ? (uint32_t)(g.ct + 1) / (uint32_t)kWinChunks : kNoWin;
-#ifdef DQDK_DIAG_SHNONE  // timing diagnostic only: the hand-off geometry without the register dword (phase B reads it)
-        sh = false;
-#endif
         lf.pk2 = tw | (mw << 11) | (((uint32_t)g.keep & 31u) << 22) | ((sh && stream ? 1u : 0u) << 27);
         lf.ct = sh ? (int)hw : g.ct;  // (sh frames never need ct: see parse_frame)
     }
@@ -840,9 +841,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
                     // the frame's checksum word sum to its LDS slot: every lane adds into
                     // one address (inline asm: the compiler's atomic optimizer would turn
                     // a uniform-address atomicAdd into a 64-step readlane loop)
-#ifndef DQDK_DIAG_NOLDS
                     frame_sum_add(&lds.sum[wslot0 + jp], &lds.sink[lane], acc0 + acc1, (lane & 15) == 15);
-#endif
                     acc0 = acc1 = 0;
                     wp = 0;
                     pmask &= pmask - 1;
@@ -1093,6 +1092,9 @@ __device__ __forceinline__ void fold_publish(const RxArgs& a, FusedLds& lds, int
                 atomicAdd(&cum[k], (unsigned long long)c[k]);
         }
         cum[11] = fail;  // first_abort_idx of this batch
+#pragma unroll
+        for (int k = 1 + 12; k < 17; k++)  // (the rest of the per-batch words the unfolded decode resets)
+            a.batch_scratch[k] = 0;
         *a.ticket = 0;
     }
 }
@@ -1342,11 +1344,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
                 const uint32_t k2 = 3u * lane + 2u < fj ? v[q][2] & kTripleMask : 0u;
                 const u32x2 t = {k0 | (k1 << kL1Shift), (k1 >> (32 - kL1Shift)) | (k2 << (2 * kL1Shift - 32))};
                 const uint32_t o = (bsj / 3u + (uint32_t)lane) * 8u;
-#ifndef DQDK_DIAG_FNOSTORE  // timing diagnostic only: the flush without its stores
                 __builtin_amdgcn_raw_buffer_store_b64(t, prs, 3u * lane < fj ? o : kOOB, 0, DQDK_FST_AUX);
-#else
-                asm volatile("" ::"v"(t.x), "v"(t.y), "v"(o), "s"(fj));
-#endif
             }
         }
     }
@@ -1414,16 +1412,16 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     // this block's private overflow region (ovf_blk_cap keys, then the table)
     uint32_t* const ovf_blk = a.ovf_blk + (uint64_t)blockIdx.x * a.ovf_blk_cap;
     const __amdgpu_buffer_rsrc_t ovf_rsrc = uniform_rsrc(ovf_blk, (uint64_t)a.ovf_blk_cap * 4u);
-    if (blockIdx.x == 0 && tid < 17)
-        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
+    // per-batch state reset -- with the counters folded, the last block's
+    // fold_publish writes every one of these words instead: two blocks' plain
+    // stores to one line, on different XCDs (each its own L2), would leave
+    // the value to whichever L2 writes back last (advisor, round 4)
+    if (!a.fold && blockIdx.x == 0 && tid < 17)
+        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;
 
     const uint32_t ntiles = (a.n + 63) / 64;
     const uint32_t nsuper = (ntiles + kFWaves - 1) / kFWaves;
     const int W = (int)a.round_windows;
-#ifdef DQDK_DIAG_TIMING
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
-    uint64_t t_a = 0, t_f = 0, t_w1 = 0, t_fw = 0;
-#endif
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
         const uint32_t tile = st * kFWaves + wave;
@@ -1434,9 +1432,6 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         const bool live = i < a.n;
 
         // ---- phase A ----
-#ifdef DQDK_DIAG_TIMING
-        const uint64_t ta0 = __builtin_amdgcn_s_memtime();
-#endif
         FrameInfo fi;
         dqdk_gpu_rx_result_t r;
         LaneFrame lf;
@@ -1447,9 +1442,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (kHeadA && __ballot(na != 0)) {
             // (the stage holds at most the last round's carry here: room for
             // these keys, at most 7 per frame, is in the round sizing)
-#ifndef DQDK_DIAG_NOASTAGE  // timing diagnostic only: phase A's keys dropped
             fused_keys_a(a, akey, na, wslot0 + (uint32_t)lane, lds, ovf_rsrc, (uint32_t)lane);
-#endif
         }
         const uint64_t smask0 = __ballot(stream);
         const int total = smask0 ? (int)wave_sum_dpp(pk_nwin(lf.pk1)) : 0;
@@ -1462,9 +1455,6 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             tmax = max(tmax, (int)lds.wtot[w]);
         const int rounds = (tmax + W - 1) / W;  // the same for every wave: the barriers below match
         lds_barrier();                          // wtot is rewritten by the next super-tile
-#ifdef DQDK_DIAG_TIMING
-        t_a += __builtin_amdgcn_s_memtime() - ta0;
-#endif
 
         // ---- phase B: rounds of W windows, the block's stage flushed after each ----
         const uint32_t lane16 = (uint32_t)lane * 16u;
@@ -1474,11 +1464,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         __amdgpu_buffer_rsrc_t lrs = frame_rsrc(lf, jl);
         // (kHeadA) lane 0 of a sh frame's first window loads 4 B further: its
         // chunk's first dword lies in the line phase A read (PFrame::hw)
-#ifdef DQDK_DIAG_SHLOAD0  // timing diagnostic only: lane 0 loads at the grid offset (wrong bytes)
-        const uint32_t lsh_lane = 0u;
-#else
         const uint32_t lsh_lane = kHeadA && lane == 0 ? 4u : 0u;
-#endif
         uint32_t lsh = kHeadA && smask0 ? (rdl(lf.pk2, jl) >> 27) & 1u : 0u;
         auto issue = [&](u32x4& d0, u32x4& d1) {
             const uint32_t vo = lane16 + (lmask != 0 ? wl * kWinBytes + (wl == 0 && lsh ? lsh_lane : 0u) : kOOB);
@@ -1564,27 +1550,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 issue(b0[d], b1[d]);
             }
-#ifdef DQDK_DIAG_FNOFLUSH  // timing diagnostic only: no flush inside the rounds (keys lost)
-            if (false) {
-#else
             if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
-#endif
-#ifdef DQDK_DIAG_TIMING
-                const uint64_t tf0 = __builtin_amdgcn_s_memtime();
-#endif
                 lds_barrier();
-#ifdef DQDK_DIAG_TIMING
-                const uint64_t tf1 = __builtin_amdgcn_s_memtime();
-                t_w1 += tf1 - tf0;
-#endif
                 fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, false);
-#ifdef DQDK_DIAG_TIMING
-                t_fw += __builtin_amdgcn_s_memtime() - tf1;
-#endif
                 lds_barrier();
-#ifdef DQDK_DIAG_TIMING
-                t_f += __builtin_amdgcn_s_memtime() - tf0;
-#endif
             }
         }
 
@@ -1631,28 +1600,22 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         if (tid < kL1Buckets && lds.scnt[tid])
             atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
-#ifdef DQDK_DIAG_TIMING
-    if (lane == 0 && a.diag) {
-        atomicAdd(&a.diag[0], (unsigned long long)t_a);
-        atomicAdd(&a.diag[1], (unsigned long long)t_f);
-        atomicAdd(&a.diag[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
-        atomicAdd(&a.diag[3], 1ull);
-        atomicAdd(&a.diag[4], (unsigned long long)t_w1);
-        atomicAdd(&a.diag[5], (unsigned long long)t_fw);
-    }
-#endif
     if (a.fold)
         fold_publish(a, lds, tid);
 }
 
-template __global__ void rx_decode_fused_kernel<0, false, false>(RxArgs);
+// the shipped variants (fused_policy_default: 1 from 128 events per frame,
+// else 2); the A/B build (-DDQDK_AB_VARIANTS) holds the other six as well
 template __global__ void rx_decode_fused_kernel<0, true, false>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, false, false>(RxArgs);
+#ifdef DQDK_AB_VARIANTS
+template __global__ void rx_decode_fused_kernel<0, false, false>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, true, false>(RxArgs);
 template __global__ void rx_decode_fused_kernel<0, false, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<0, true, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, false, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, true, true>(RxArgs);
+#endif
 
 // Frames the fused decode staged but whose final status is not OK: subtract
 // their events from the table (u32 wrap: +1 then -1 leaves every bin exact).
@@ -2071,9 +2034,17 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArg
 // starts itself (a prologue over L2-resident counts, in place of a launch of
 // its own), and block 0 publishes each bucket's first item for the slice pass.
 //
-// Per key: one buffer load, one returning LDS add (counts step by 2, so the
-// returned rank is the key's byte offset inside its slice run), the rank
-// through LDS, one LDS read of the run start, one u16 LDS store.  The next
+// The item is a two-pass counting sort over per-lane-slot counters: slice s
+// has 32 counters, cnt[s][l & 31], one per lane position of a 32-lane LDS
+// group, so the 32 lanes of a group always add to 32 different banks (a
+// random slice per lane over one counter per slice made 53 % of the LDS
+// cycles bank conflicts and serialised same-slice adds: profiles/r04g).  Per
+// key: one buffer load, one non-returning LDS add (count), a block-wide scan
+// of the 4096 counters into run cursors (slice-major, so slice s's keys are
+// the contiguous concatenation of its 32 sub-runs; the order inside a slice
+// run is immaterial to the slice pass), one returning LDS add on the
+// key's cursor (its byte offset in the stage) and one u16 LDS store.  Slots
+// past the item and triple pads are masked off (no stage slot).  The next
 // item's keys load while this one is written out.  The barriers hand off LDS
 // data only (global reads are read-only inputs, global writes are not read
 // back by the block): lds_barrier() keeps the next item's key loads in flight
@@ -2089,18 +2060,16 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     constexpr int kJT = kPartKeysPerThread / 3;                      // triple loads per lane (gathered items)
     constexpr uint32_t kWaveKeys = (uint32_t)kPartChunk / kPWaves;     // 960 key slots per wave
     constexpr uint32_t kWaveTriples = kWaveKeys / 3;                  // 320 triple slots per wave
-    constexpr uint32_t kDummy = 1u << kL1Shift;  // a slot past the item or a triple's pad: counter 128
-    constexpr int kRankWords = (kPartKeysPerThread + 1) / 2;
-    __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk];
-    // counters / run starts: [0, 128) the slices, 128 the dummy slice
-    __shared__ __attribute__((aligned(16))) uint32_t lcnt[2 * kSubs];
-    __shared__ __attribute__((aligned(16))) uint32_t loff[2 * kSubs];
-    __shared__ uint32_t rnk[kRankWords * kPartThreads];  // count() -> scatter()
+    constexpr uint32_t kDummy = 1u << kL1Shift;  // a slot past the item or a triple's pad (no stage slot)
+    constexpr int kCtr = kSubs * 32;             // counters: [slice][lane & 31]
+    static_assert(kCtr == 4 * kPartThreads, "the scan takes four counters per thread");
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk + 2];  // + the dummies' sink
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[kCtr];  // counts (x2: bytes), zero between items
+    __shared__ __attribute__((aligned(16))) uint32_t cur[kCtr];  // run cursors (byte offsets in the stage)
     __shared__ uint32_t prt[2][kMaxFusedGrid + 1], prk[2][kMaxFusedGrid + 1];  // piece starts: triples, keys
     __shared__ uint32_t s_cnt[kMaxSeg], s_base8[kMaxSeg], ist[kMaxSeg + 1];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t wsum[kPWaves];
-    __shared__ uint32_t s_nv;  // valid keys of the current item
     const int tid = threadIdx.x;
     const uint32_t lane = (uint32_t)tid & 63u, wave = rfl((uint32_t)tid >> 6);
     const bool fused = a.fused != 0;
@@ -2108,8 +2077,7 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
 
     // ---- prologue: segments (size, input index) and their first items ----
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
-    if (tid < 2 * kSubs)
-        lcnt[tid] = 0;
+    ((u32x4_t*)cnt)[tid] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
     uint32_t nit = 0;
     if ((uint32_t)tid < nseg) {
@@ -2174,8 +2142,9 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     // a gathered item: its bucket's piece starts (then a barrier)
     auto stage_pieces = [&](const Item& g, int pb) {
         if (g.gath && (uint32_t)tid <= a.fgrid) {
-            prt[pb][tid] = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + tid];
-            prk[pb][tid] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + tid];
+            const uint32_t t = opaque((uint32_t)tid);
+            prt[pb][t] = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + t];
+            prk[pb][t] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + t];
         }
     };
     // slots: gathered items, wave w takes the item's triples [320w, 320w +
@@ -2184,12 +2153,6 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     // (a gathered item's triple j loads into key[2j], key[2j + 1] and is
     // unpacked in place, from the last triple down)
     uint32_t key[kPartKeysPerThread];
-#ifndef DQDK_P2_RREG  // 1: the ranks stay in registers from count() to scatter() (A/B)
-#define DQDK_P2_RREG 0
-#endif
-#if DQDK_P2_RREG
-    uint32_t rr[kRankWords];
-#endif
     uint32_t pad = 0;  // gathered: bit 2j + i set = key 3j + 2 - i is a pad of its piece's last triple
     auto load = [&](const Item& g, int pb) {
         pad = 0;
@@ -2246,14 +2209,10 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
                 key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wave * kWaveKeys + lane) * 4u, j * 256, kLdAux);
         }
     };
-    // count: every key (bucket-local, 21 bits) gets its slice counter (LDS
-    // address (key >> 12) & 0x3fc) raised by 2; the returned count is the
-    // key's byte offset in its slice run.  The ranks go to LDS (two u16 per
-    // word, [pair][thread]: conflict-free), the key becomes (counter address
-    // << 16) | its low 16 bits, all that scatter() needs of it (in registers
-    // with the ranks, the scan's registers would spill, and a spill reload
-    // waits for every key load in flight).  Slots past the item and pads
-    // become the dummy key (bit 21: counter 128).
+    // count: every key (bucket-local, 21 bits) raises its slice's counter of
+    // the lane's slot, cnt[(key >> 14) & 127][lane & 31], by 2 (bytes of a
+    // u16); the key becomes (counter byte address << 16) | its low 16 bits,
+    // all that scatter() needs of it.  Slots past the item and pads add 0.
     auto count = [&](const Item& g) {
         if (g.gath) {
 #pragma unroll
@@ -2271,9 +2230,14 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
                 }
             }
             if (wave * kWaveTriples + kWaveTriples > g.nu) {
+                // (the lane term opaque: hoisted per j out of the item loop,
+                // the compares' operands would stay live, and spill)
+                uint32_t ln = lane;
+                asm volatile("" : "+v"(ln));
+                const int32_t lim = (int32_t)g.nu - (int32_t)(wave * kWaveTriples);
 #pragma unroll
                 for (int j = 0; j < kJT; j++) {
-                    const bool v = wave * kWaveTriples + 64u * (uint32_t)j + lane < g.nu;
+                    const bool v = (int32_t)ln < lim - 64 * j;
 #pragma unroll
                     for (int i = 0; i < 3; i++)
                         key[3 * j + i] = v ? key[3 * j + i] : kDummy;
@@ -2281,58 +2245,75 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             }
         } else {
             const bool tail = wave * kWaveKeys + kWaveKeys > g.nu;
+            uint32_t ln = lane;
+            asm volatile("" : "+v"(ln));
+            const int32_t lim = (int32_t)g.nu - (int32_t)(wave * kWaveKeys);
 #pragma unroll
             for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = !tail || wave * kWaveKeys + 64u * (uint32_t)j + lane < g.nu ? key[j] & kTripleMask : kDummy;
+                key[j] = !tail || (int32_t)ln < lim - 64 * j ? key[j] & kTripleMask : kDummy;
         }
+        // a dummy adds 0 to its lane's counter of slice 0 (no branch) and is
+        // marked by bit 31 for scatter()
+        const uint32_t sub4 = (lane & 31u) << 2;
 #pragma unroll
-        for (int h = 0; h < kPartKeysPerThread; h += 8) {
-            constexpr int kH = 8;
-            uint32_t r[kH];
-#pragma unroll
-            for (int j = 0; j < kH; j++) {
-                if (h + j < kPartKeysPerThread) {
-                    const uint32_t sa = (key[h + j] >> (kSliceBits - 2)) & ((2 * kSubs - 1) << 2);
-                    r[j] = atomicAdd(&lcnt[sa >> 2], 2u);
-                    key[h + j] = __builtin_amdgcn_perm(sa, key[h + j], 0x05040100u);  // sa.lo16 : key.lo16
-                } else {
-                    r[j] = 0;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kH / 2; j++)
-#if DQDK_P2_RREG
-                if (h / 2 + j < kRankWords)
-                    rr[h / 2 + j] = r[2 * j] | (r[2 * j + 1] << 16);
-#else
-                rnk[(h / 2 + j) * kPartThreads + tid] = r[2 * j] | (r[2 * j + 1] << 16);
-#endif
+        for (int j = 0; j < kPartKeysPerThread; j++) {
+            // slice * 128 + (lane & 31) * 4: the counter's byte address
+            const uint32_t ca = ((key[j] >> (kSliceBits - 7)) & ((kSubs - 1) << 7)) | sub4;
+            const uint32_t d = key[j] >> kL1Shift;  // 1: dummy
+            __hip_atomic_fetch_add(&cnt[ca >> 2], 2u - 2u * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            key[j] = __builtin_amdgcn_perm(ca, key[j], 0x05040100u) | (d << 31);  // ca.lo16 : key.lo16
+            // (opaque: scatter() re-derives the counter and increment from the
+            // key; kept live across the scan they would spill)
+            asm volatile("" : "+v"(key[j]));
         }
     };
-    // scatter: each key's u16 to its slice run in the stage, at the run start
-    // (after the scan, loff) + its rank (the dummy slots land past the valid
-    // keys).  Every LDS read of a round is issued before its first use.
+    // scan: the counters (slice-major) into run cursors, four per thread;
+    // the counts are zeroed for the next item.  Returns the item's valid
+    // keys; item's 129 run starts (u16 offsets) go to runs.
+    auto scan = [&](uint32_t item) -> uint32_t {
+        const u32x4_t c = ((const u32x4_t*)cnt)[tid];
+        uint32_t z = 0;
+        asm volatile("" : "+v"(z));  // (a zero vector hoisted out of the item loop spills)
+        ((u32x4_t*)cnt)[tid] = u32x4_t{z, z, z, z};
+        const uint32_t sum = c.x + c.y + c.z + c.w;
+        const uint32_t incl = wave_incl_scan_dpp(sum);
+        if (lane == 63)
+            wsum[wave] = incl;
+        lds_barrier();
+        uint32_t woff = 0, tot = 0, wv = wave;
+        asm volatile("" : "+s"(wv));  // (else 16 compare masks stay live across the item loop)
+#pragma unroll
+        for (int w = 0; w < kPWaves; w++) {
+            const uint32_t x = wsum[w];
+            woff += (uint32_t)w < wv ? x : 0u;
+            tot += x;
+        }
+        const uint32_t ex = woff + incl - sum;
+        ((u32x4_t*)cur)[tid] = u32x4_t{ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
+        uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
+        if ((tid & 7) == 0)
+            ro[opaque((uint32_t)tid) >> 3] = (uint16_t)(ex / 2);
+        if (tid == 0)
+            ro[kSubs] = (uint16_t)(tot / 2);
+        return tot / 2;
+    };
+    // scatter: each key's u16 to the stage at its counter's cursor (a
+    // returning add); every add of a round of 8 is issued before the first
+    // store that uses one.
     auto scatter = [&]() {
         uint8_t* const st8 = (uint8_t*)stage;
 #pragma unroll
         for (int h = 0; h < kPartKeysPerThread; h += 8) {
-            uint32_t o[8], rk[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#if DQDK_P2_RREG
-                rk[j] = h / 2 + j < kRankWords ? rr[h / 2 + j] : 0u;
-#else
-                rk[j] = rnk[(h / 2 + j) * kPartThreads + tid];
-#endif
+            uint32_t o[8];
 #pragma unroll
             for (int j = 0; j < 8; j++)
                 if (h + j < kPartKeysPerThread)
-                    o[j] = *(const uint32_t*)((const uint8_t*)loff + (key[h + j] >> 16));
+                    o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtr - 1)], 2u - 2u * (key[h + j] >> 31),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                if (h + j < kPartKeysPerThread)
-                    *(uint16_t*)(st8 + o[j] + ((j & 1) ? rk[j / 2] >> 16 : rk[j / 2] & 0xffffu)) =
-                        (uint16_t)key[h + j];
+                if (h + j < kPartKeysPerThread)  // a dummy's u16 goes to the sink past the stage
+                    *(uint16_t*)(st8 + ((key[h + j] >> 31) ? (uint32_t)kPartChunk * 2u : o[j])) = (uint16_t)key[h + j];
         }
     };
 
@@ -2347,29 +2328,7 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
         count(g);
         lds_barrier();
-        // wave 0: run starts (byte offsets in the stage), the slices first,
-        // then the dummy counter; the item's run offsets and valid keys; the
-        // counts are zeroed for the next item
-        if (wave == 0) {
-            const u32x4_t c = ((const u32x4_t*)lcnt)[lane];  // counters 4 lane .. 4 lane + 3
-            uint32_t z = 0;
-            asm volatile("" : "+v"(z));  // (a zero vector hoisted out of the item loop spills)
-            ((u32x4_t*)lcnt)[lane] = u32x4_t{z, z, z, z};
-            const uint32_t sum = c.x + c.y + c.z + c.w;
-            const uint32_t ex = wave_incl_scan_dpp(sum) - sum;
-            const u32x4_t o4 = {ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
-            ((u32x4_t*)loff)[lane] = o4;
-            uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
-            if (lane < kSubs / 4) {
-                ro[4 * lane] = (uint16_t)(o4.x / 2);
-                ro[4 * lane + 1] = (uint16_t)(o4.y / 2);
-                ro[4 * lane + 2] = (uint16_t)(o4.z / 2);
-                ro[4 * lane + 3] = (uint16_t)(o4.w / 2);
-            } else if (lane == kSubs / 4) {
-                ro[kSubs] = (uint16_t)(ex / 2);
-                s_nv = ex / 2;
-            }
-        }
+        const uint32_t nv = scan(item);
         lds_barrier();
         scatter();
         // the next item's keys load while this one is written out
@@ -2379,17 +2338,16 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             stage_pieces(g, pb ^ 1);
         }
         lds_barrier();
-        const uint32_t nv = s_nv;
         if (more)
             load(g, pb ^ 1);
         // item i's valid keys go to part2 [i * kPartChunk, + nv) in 16-B stores
-        // (the dummy keys of the last group are never read)
+        // (the bytes past nv in the last store are never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;
         u32x4_t* dst4 = (u32x4_t*)(a.part2 + (uint64_t)item * kPartChunk);
-        for (uint32_t p = tid; p * 8u < nv; p += kPartThreads)
+        for (uint32_t p = opaque((uint32_t)tid); p * 8u < nv; p += kPartThreads)
             dst4[p] = st4[p];
-        // (no barrier here: the stage and s_nv are rewritten only after the
-        // next item's first barrier)
+        // (no barrier here: the stage is rewritten, and wsum and the cursors
+        // re-read, only after the next item's first barrier)
     }
     if (a.p2_ticket) {
         // every block read the counters in its prologue: the last one to

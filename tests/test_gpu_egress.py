@@ -390,17 +390,21 @@ def test_raw_stream_fused_batches_counter_delta(tmp_path, deferred):
     """Host drop-in with a raw fd on partitioned energy-histo batches: the
     fused decode sums the per-packet counters itself (no rx_count), and the
     call's counter delta, results, raw stream and the table all equal the
-    oracle's, batch by batch."""
+    oracle's, batch by batch.  The batch sizes alternate between 40 decode
+    blocks and 3-5: the delta is published by the last block alone (a reset
+    by block 0 in the same launch, on another XCD's L2, raced it: advisor r4),
+    and a short batch after a long one must not read the long one's words."""
     _need_gpu()
     cfg = D.RxConfig(payloadsz=1458, mode=D.MODE_ENERGYHISTO, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
     path = tmp_path / "raw.bin"
     fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     want, okeys_all, ores_all = [], [], []
-    q = D.RxQueue(0, cfg, 4096)
+    sizes = [4096, 40000, 2100, 40000, 5000]
+    q = D.RxQueue(0, cfg, max(sizes))
     try:
         q.set_raw_fd(fd, deferred=deferred)
-        for b in range(3):
-            umem, desc = D.synth_umem(4096, 1500, 4096, queue=b, faulty=True)
+        for b, n in enumerate(sizes):
+            umem, desc = D.synth_umem(n, 1500, 4096, queue=b, faulty=True)
             ores, ocnt, okeys = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
             res, delta = q.process_batch(umem, desc)
             np.testing.assert_array_equal(res, ores)

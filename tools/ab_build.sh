@@ -19,7 +19,7 @@ done
 objs=""
 for f in $src/dqdk_amd/csrc/*.hip; do
     o=$src/$(basename $f .hip).o
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $EXTRA_FLAGS -c $f -o $o
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DDQDK_AB_VARIANTS $EXTRA_FLAGS -c $f -o $o
     objs="$objs $o"
 done
 for f in $src/dqdk_amd/csrc/*.c; do
