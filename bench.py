@@ -199,6 +199,15 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
 
     for _ in range(args.warmup):
         step()
+    # the queue's staging placement probe (include/dqdk_gpu.h: its first 2 x 3
+    # fused batches try candidate piece buffers, the next keeps the fastest)
+    # belongs to the warmup: extra untimed batches until it has decided
+    warm_extra = 0
+    while q.staging_probe()["chosen"] < 0 and warm_extra < 8 and n >= 65536 and histo and E and \
+            not pass_records:
+        step()
+        warm_extra += 1
+    probe = q.staging_probe()
     q.flush_histogram()  # no warmup batch left staged for the timed region's slice passes
     torch.cuda.synchronize(dev)
     q.read_timing()  # discard
@@ -395,6 +404,9 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         "histogram": histogram,
         "roofline": roofline,
         "cpu_baseline": cpu,
+        # the staging placement probe: kept candidate piece buffer, each
+        # candidate's decode ns per frame, untimed warmup batches it added
+        "staging_probe": dict(probe, warmup_extra=warm_extra),
     }
 
 

@@ -124,6 +124,7 @@ SIGNATURES = {
     "dqdk_gpu_histogram_flush": (C.c_int, [_P]),
     "dqdk_gpu_histogram_batches_per_pass": (C.c_int, [_P]),
     "dqdk_gpu_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
+    "dqdk_gpu_queue_staging_probe": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int]),
     "dqdk_gpu_timing_stage_name": (C.c_char_p, [C.c_int]),
     "dqdk_gpu_last_error": (C.c_char_p, []),
     "dqdk_synth_umem_size": (C.c_uint64, [C.POINTER(SynthCfg), C.c_uint32]),

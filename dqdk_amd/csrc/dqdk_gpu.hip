@@ -85,6 +85,9 @@ constexpr int kPart2TicketWord = 22;  // rx_part2's last block re-zeroes the slo
 // The fused pieces' offset inside their allocation can move by up to this
 // many words (placement relative to the frames: DESIGN.md §5)
 constexpr uint64_t kPieceShiftMax = 8u << 20;  // 32 MiB
+constexpr int kProbeCands = DQDK_GPU_PROBE_CANDS;  // staging placement probe: candidate piece buffers
+constexpr int kProbeSteps = 2 * kProbeCands;  // each candidate once untimed (first touch), then once timed
+constexpr uint32_t kProbeMinFrames = 65536;
 
 uint32_t events_per_payload(uint32_t mode, uint32_t payloadsz)  // src/tristan.c:72-85
 {
@@ -211,6 +214,20 @@ struct dqdk_gpu_queue {
     uint32_t fmap = 0;             // DQDK_GPU_FRAME_MAP=1: interleaved fused frame map
     bool p2zero_off = false;       // DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch
     bool small_off = false;        // DQDK_GPU_SMALL=0: small batches take the three-launch form too
+    // Staging placement probe: the fused decode's rate
+    // depends on where its piece buffer (d_part1, the decode's write stream)
+    // lands physically relative to the image it reads -- 2.12 vs 2.35 ms at
+    // 1M x 9000 B, same build, same image.  The first fused batches of at
+    // least kProbeMinFrames frames run on kProbeCands candidate allocations
+    // in turn (each first untimed, its pages' first use, then timed); the fastest is
+    // kept and the others freed.  DQDK_GPU_STAGING_PROBE=0: off.
+    int probe = 0;                 // next probe step (1-based), 0: off or done
+    uint32_t* part1_cand[kProbeCands] = {};
+    float probe_ms[kProbeCands] = {};  // min decode ms per frame x 1e6 of each candidate
+    int probe_timed = -1;          // candidate of the batch whose events are pending
+    uint32_t probe_n = 0;          // its frames
+    hipEvent_t probe_ev[2] = {nullptr, nullptr};
+    int probe_chosen = -1;         // -1: not decided
     int alloc_kind = 0;            // device memory of the table and staging (dev_alloc)
     // Partitioned batches stage their slice-sorted keys (part2 + runs +
     // scratch, one slot each); the slice pass -- which sweeps the low-byte
@@ -524,6 +541,72 @@ int clean_slot(dqdk_gpu_queue* q, uint32_t* slot_scratch)
     return 0;
 }
 
+// Staging placement probe, before a fused batch of n frames: collects the
+// previous probe batch's decode time, decides once every step is timed, and
+// points d_part1 (and the overflow regions inside it) at this batch's
+// candidate.  Returns the candidate to time (-1: none).
+int probe_step(dqdk_gpu_queue* q, uint32_t n)
+{
+    if (q->probe_timed >= 0) {
+        float ms = 0;
+        hipError_t e = hipEventSynchronize(q->probe_ev[1]);
+        if (e == hipSuccess)
+            e = hipEventElapsedTime(&ms, q->probe_ev[0], q->probe_ev[1]);
+        if (e != hipSuccess)
+            return fail("staging probe: decode events", e);
+        const float per = ms * 1e6f / (float)q->probe_n;
+        float& best = q->probe_ms[q->probe_timed];
+        best = best > 0 ? std::min(best, per) : per;
+        q->probe_timed = -1;
+    }
+    if (!q->probe || n < kProbeMinFrames || !q->fused_elems)
+        return -1;
+    if (q->probe > kProbeSteps) {  // every candidate timed: keep the fastest
+        int c = 0;
+        for (int k = 1; k < kProbeCands; k++)
+            if (q->part1_cand[k] && q->probe_ms[k] > 0 && q->probe_ms[k] < q->probe_ms[c])
+                c = k;
+        q->probe_chosen = c;
+        q->d_part1 = q->part1_cand[c];
+        q->d_ovf_blk = q->d_part1 + q->piece_shift + q->fused_elems;
+        for (int k = 1; k < kProbeCands; k++)  // (the original, candidate 0, stays if not chosen: freed with the queue)
+            if (k != c) {
+                dev_free(q->part1_cand[k]);
+                q->part1_cand[k] = nullptr;
+            }
+        if (c != 0) {
+            dev_free(q->part1_cand[0]);
+            q->part1_cand[0] = nullptr;
+        }
+        q->probe = 0;
+        return -1;
+    }
+    if (q->probe == 1) {  // the candidates, allocated beside the original (other physical pages)
+        q->part1_cand[0] = q->d_part1;
+        for (int k = 1; k < kProbeCands; k++)
+            if (dev_alloc(&q->part1_cand[k], q->part1_elems * 4, q->alloc_kind) != hipSuccess) {
+                (void)hipGetLastError();
+                q->part1_cand[k] = nullptr;
+            }
+        if ((!q->probe_ev[0] && hipEventCreate(&q->probe_ev[0]) != hipSuccess) ||
+            (!q->probe_ev[1] && hipEventCreate(&q->probe_ev[1]) != hipSuccess)) {
+            (void)hipGetLastError();
+            q->probe = 0;
+            return -1;
+        }
+    }
+    const int step = q->probe++;
+    int c = (step - 1) % kProbeCands;
+    if (!q->part1_cand[c])
+        c = 0;  // (a candidate that did not allocate)
+    q->d_part1 = q->part1_cand[c];
+    q->d_ovf_blk = q->d_part1 + q->piece_shift + q->fused_elems;
+    if (step <= kProbeCands)
+        return -1;  // the candidate's first batch: untimed
+    q->probe_n = n;
+    return c;
+}
+
 // The fused decode variant of a policy (fused_policy_default; the variants
 // kFusedPolicies does not hold are not in this build's code object).
 void (*fused_kernel(uint32_t pol))(RxArgs)
@@ -570,6 +653,7 @@ int read_knobs(dqdk_gpu_queue* q)
     q->fmap = env("DQDK_GPU_FRAME_MAP") ? (uint32_t)(atoi(env("DQDK_GPU_FRAME_MAP")) != 0) : 0u;
     q->p2zero_off = env("DQDK_GPU_P2ZERO") && !strcmp(env("DQDK_GPU_P2ZERO"), "0");
     q->small_off = env("DQDK_GPU_SMALL") && !strcmp(env("DQDK_GPU_SMALL"), "0");
+    q->probe = env("DQDK_GPU_STAGING_PROBE") && !strcmp(env("DQDK_GPU_STAGING_PROBE"), "0") ? 0 : 1;
     if (const char* v = env("DQDK_GPU_PIECE_SHIFT"))  // KiB (tools/state_probe.py)
         q->piece_shift = std::min<uint64_t>((uint64_t)atoll(v) * 256u, kPieceShiftMax - 256u) & ~63ull;
     return 0;
@@ -626,6 +710,9 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     ca.ticket = (uint32_t*)(q->d_batch + kTicketWord);
 
     if (fused) {
+        const int probe_c = probe_step(q, n);
+        if (probe_c < -1)
+            return probe_c;
         ra.keys = nullptr;  // no frame-order records
         ra.scratch = slot_scratch;
         ra.part1 = q->d_part1 + q->piece_shift;
@@ -654,7 +741,14 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         auto kern = fused_kernel(q->fused_pol);
         if (!kern)
             return fail_errno(-EINVAL, "fused decode: no such variant");
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+        if (probe_c >= 0) {
+            HIPCHK(hipEventRecord(q->probe_ev[0], q->stream));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+            HIPCHK(hipEventRecord(q->probe_ev[1], q->stream));
+            q->probe_timed = probe_c;
+        } else {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(kFThreads), 0, q->stream, ra);
+        }
     } else if (n <= (uint32_t)kTile && !q->small_off) {
         // one block: decode, abort and count in a single launch (rx_small),
         // the frames spread over all its waves (a 64-frame batch is four
@@ -870,13 +964,22 @@ int raw_write_pending(dqdk_gpu_queue* q, int k)
     return write_fd(q->raw_fd, q->h_rawb[k], q->raw_pend_len[k]);
 }
 
-// every batch's raw stream written (older buffer first)
+// every batch's raw stream written (older buffer first).  Both D2H copies
+// are waited for even when the first write() fails: nothing may still be in
+// flight into h_rawb once this returns (destroy frees it next; a copy landing
+// in freed pinned memory is a GPU fault reported at some later copy, DESIGN
+// section 3)
 int raw_drain(dqdk_gpu_queue* q)
 {
     const int last = (int)((q->raw_seq + 1) & 1);  // buffer of the most recent batch
     int rc = raw_write_pending(q, last ^ 1);
     if (!rc)
         rc = raw_write_pending(q, last);
+    if (q->raw_stream) {
+        const hipError_t e = hipStreamSynchronize(q->raw_stream);  // (an unwritten batch stays pending)
+        if (!rc && e != hipSuccess)
+            rc = fail("raw egress: hipStreamSynchronize", e);
+    }
     return rc;
 }
 
@@ -1168,7 +1271,13 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     (void)hipFree(q->d_batch);
     (void)hipFree(q->d_blkcnt);
     dev_free(q->d_keys);
+    for (int k = 0; k < kProbeCands; k++)
+        if (q->part1_cand[k] && q->part1_cand[k] != q->d_part1)
+            dev_free(q->part1_cand[k]);
     dev_free(q->d_part1);
+    for (auto ev : q->probe_ev)
+        if (ev)
+            (void)hipEventDestroy(ev);
     dev_free(q->d_part1_rec);
     (void)hipFree(q->d_ovf);
     dev_free(q->d_part2);
@@ -1527,6 +1636,17 @@ int dqdk_gpu_timing_stages(dqdk_gpu_queue_t* q, uint32_t stage_mask)
         return -EINVAL;
     q->stage_mask = stage_mask;
     return 0;
+}
+
+int dqdk_gpu_queue_staging_probe(dqdk_gpu_queue_t* q, int* chosen, float* ns_per_frame, int ncand)
+{
+    if (!q)
+        return -EINVAL;
+    if (chosen)
+        *chosen = q->probe_chosen;
+    for (int k = 0; ns_per_frame && k < ncand && k < kProbeCands; k++)
+        ns_per_frame[k] = q->probe_ms[k];
+    return kProbeCands;
 }
 
 int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages)

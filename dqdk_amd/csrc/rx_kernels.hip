@@ -2150,9 +2150,13 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     // slots: gathered items, wave w takes the item's triples [320w, 320w +
     // 320), 64 per load (load j: triple 320w + 64j + lane -> keys 3j .. 3j + 2
     // of the lane); contiguous items, keys [960w, 960w + 960), 64 per load
-    // (a gathered item's triple j loads into key[2j], key[2j + 1] and is
-    // unpacked in place, from the last triple down)
-    uint32_t key[kPartKeysPerThread];
+    // (a gathered item's triple j loads into nk[2j], nk[2j + 1] and is
+    // unpacked into key[3j .. 3j + 2] by count()).  A gathered item's loads
+    // are issued a phase early: they land in nk while the previous item is
+    // scanned, scattered and written out; a contiguous item's 15 keys (rx_part1
+    // runs, rare on the fused path) load into key once the previous item's
+    // scatter has freed it (no registers for both).
+    uint32_t key[kPartKeysPerThread], nk[2 * kJT];
     uint32_t pad = 0;  // gathered: bit 2j + i set = key 3j + 2 - i is a pad of its piece's last triple
     auto load = [&](const Item& g, int pb) {
         pad = 0;
@@ -2198,16 +2202,16 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
                     }
                 }
                 const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(src, u, 512 * j, kLdAux);
-                key[2 * j] = v.x;
-                key[2 * j + 1] = v.y;
+                nk[2 * j] = v.x;
+                nk[2 * j + 1] = v.y;
             }
-        } else {
-            const __amdgpu_buffer_rsrc_t src =
-                uniform_rsrc(a.part1 + (uint64_t)g.base8 * kBucketAlign, (uint64_t)g.nu * 4u);
-#pragma unroll
-            for (int j = 0; j < kPartKeysPerThread; j++)
-                key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wave * kWaveKeys + lane) * 4u, j * 256, kLdAux);
         }
+    };
+    auto load_contig = [&](const Item& g) {
+        const __amdgpu_buffer_rsrc_t src = uniform_rsrc(a.part1 + (uint64_t)g.base8 * kBucketAlign, (uint64_t)g.nu * 4u);
+#pragma unroll
+        for (int j = 0; j < kPartKeysPerThread; j++)
+            key[j] = __builtin_amdgcn_raw_buffer_load_b32(src, (wave * kWaveKeys + lane) * 4u, j * 256, kLdAux);
     };
     // count: every key (bucket-local, 21 bits) raises its slice's counter of
     // the lane's slot, cnt[(key >> 14) & 127][lane & 31], by 2 (bytes of a
@@ -2217,7 +2221,7 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         if (g.gath) {
 #pragma unroll
             for (int j = kJT - 1; j >= 0; j--) {
-                const uint32_t x = key[2 * j], y = key[2 * j + 1];
+                const uint32_t x = nk[2 * j], y = nk[2 * j + 1];
                 key[3 * j] = x & kTripleMask;
                 key[3 * j + 1] = __builtin_amdgcn_alignbit(y, x, kL1Shift) & kTripleMask;
                 key[3 * j + 2] = y >> (2 * kL1Shift - 32);
@@ -2280,14 +2284,9 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         if (lane == 63)
             wsum[wave] = incl;
         lds_barrier();
-        uint32_t woff = 0, tot = 0, wv = wave;
-        asm volatile("" : "+s"(wv));  // (else 16 compare masks stay live across the item loop)
-#pragma unroll
-        for (int w = 0; w < kPWaves; w++) {
-            const uint32_t x = wsum[w];
-            woff += (uint32_t)w < wv ? x : 0u;
-            tot += x;
-        }
+        // the waves' totals, one per lane (16 unrolled reads held 32 registers)
+        const uint32_t x = lane < (uint32_t)kPWaves ? wsum[opaque(lane) & (kPWaves - 1)] : 0u;
+        const uint32_t woff = wave_sum_dpp(lane < wave ? x : 0u), tot = wave_sum_dpp(x);
         const uint32_t ex = woff + incl - sum;
         ((u32x4_t*)cur)[tid] = u32x4_t{ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z};
         uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
@@ -2301,17 +2300,21 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     // returning add); every add of a round of 8 is issued before the first
     // store that uses one.
     auto scatter = [&]() {
+#ifndef DQDK_P2_SG
+#define DQDK_P2_SG 4
+#endif
+        constexpr int kSG = DQDK_P2_SG;
         uint8_t* const st8 = (uint8_t*)stage;
 #pragma unroll
-        for (int h = 0; h < kPartKeysPerThread; h += 8) {
-            uint32_t o[8];
+        for (int h = 0; h < kPartKeysPerThread; h += kSG) {
+            uint32_t o[kSG];
 #pragma unroll
-            for (int j = 0; j < 8; j++)
+            for (int j = 0; j < kSG; j++)
                 if (h + j < kPartKeysPerThread)
                     o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtr - 1)], 2u - 2u * (key[h + j] >> 31),
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-            for (int j = 0; j < 8; j++)
+            for (int j = 0; j < kSG; j++)
                 if (h + j < kPartKeysPerThread)  // a dummy's u16 goes to the sink past the stage
                     *(uint16_t*)(st8 + ((key[h + j] >> 31) ? (uint32_t)kPartChunk * 2u : o[j])) = (uint16_t)key[h + j];
         }
@@ -2323,23 +2326,29 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         g = geo(blockIdx.x);
         stage_pieces(g, 0);
         lds_barrier();
-        load(g, 0);
+        if (g.gath)
+            load(g, 0);
+        else
+            load_contig(g);
     }
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
         count(g);
-        lds_barrier();
-        const uint32_t nv = scan(item);
-        lds_barrier();
-        scatter();
-        // the next item's keys load while this one is written out
+        // the next item's keys load while this one is scanned, scattered and
+        // written out
         const bool more = item + gridDim.x < nitems;
         if (more) {
             g = geo(item + gridDim.x);
             stage_pieces(g, pb ^ 1);
         }
         lds_barrier();
-        if (more)
+        if (more && g.gath)
             load(g, pb ^ 1);
+        const uint32_t nv = scan(item);
+        lds_barrier();
+        scatter();
+        if (more && !g.gath)
+            load_contig(g);
+        lds_barrier();
         // item i's valid keys go to part2 [i * kPartChunk, + nv) in 16-B stores
         // (the bytes past nv in the last store are never read)
         const u32x4_t* st4 = (const u32x4_t*)stage;

@@ -216,6 +216,15 @@ class RxQueue:
         L.check(L.lib().dqdk_gpu_histogram_write_csv(self._h, fd, C.byref(n)), "histogram_write_csv")
         return int(n.value)
 
+    def staging_probe(self) -> dict:
+        """The staging placement probe's outcome: the kept candidate piece
+        buffer (-1: undecided or off) and each candidate's best decode ns per
+        frame (include/dqdk_gpu.h)."""
+        ch = C.c_int(-1)
+        ns = (C.c_float * 8)()
+        k = L.check(L.lib().dqdk_gpu_queue_staging_probe(self._h, C.byref(ch), ns, 8), "staging_probe")
+        return {"chosen": ch.value, "ns_per_frame": [round(ns[i], 4) for i in range(k)]}
+
     # -- stage timing --------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:
         L.check(L.lib().dqdk_gpu_timing_enable(self._h, int(on)), "timing_enable")

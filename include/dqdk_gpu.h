@@ -389,6 +389,20 @@ int dqdk_gpu_timing_stages(dqdk_gpu_queue_t* q, uint32_t stage_mask);
 int dqdk_gpu_timing_read(dqdk_gpu_queue_t* q, double* stage_ms, uint64_t* counts, int nstages);
 const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
 
+/* ---- staging placement probe (no reference counterpart) ------------------- */
+/* The fused decode's rate depends on where its piece buffer lands physically
+ * relative to the UMEM image it reads.  A queue's first
+ * fused batches of at least 65536 frames run on DQDK_GPU_PROBE_CANDS candidate
+ * piece buffers in turn (each candidate's first batch untimed, then one more
+ * batch each, its decode timed by HIP events: 2 x DQDK_GPU_PROBE_CANDS
+ * batches); at the next such batch the fastest is kept, the others freed
+ * (DQDK_GPU_STAGING_PROBE=0 at queue creation: off).  This reads the outcome:
+ * *chosen = the kept candidate (-1: not decided yet or off), ns_per_frame[k]
+ * = candidate k's best decode time per frame (0: untimed), k < ncand.
+ * Returns the number of candidates. */
+#define DQDK_GPU_PROBE_CANDS 3
+int dqdk_gpu_queue_staging_probe(dqdk_gpu_queue_t* q, int* chosen, float* ns_per_frame, int ncand);
+
 const char* dqdk_gpu_last_error(void);
 
 /* ---- synthetic UMEM generator (bench/test input only; host C) ------------ */

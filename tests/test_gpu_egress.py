@@ -424,3 +424,42 @@ def test_raw_stream_fused_batches_counter_delta(tmp_path, deferred):
     nz = np.flatnonzero(hist)
     np.testing.assert_array_equal(nz.astype(np.uint32), u)
     np.testing.assert_array_equal(hist[nz].astype(np.uint64), c)
+
+
+@pytest.mark.parametrize("broken", [False, True], ids=["file", "broken-pipe"])
+def test_destroy_with_deferred_raw_copy_in_flight_then_new_queue(tmp_path, broken):
+    """The ordering behind round 4's illegal-address fault (DESIGN.md section
+    3): a deferred raw batch's D2H copy into the queue's pinned buffer is in
+    flight on the raw side stream when the queue is destroyed (no drain by
+    the caller; with a broken pipe the drain's write() fails first).  destroy
+    must wait for that copy before it frees the pinned buffer: a copy landing
+    in freed memory faults the GPU and is reported by some later, unrelated
+    copy.  A new queue's first batch right after then checks out against the
+    oracle, table included, and a device-wide sync reports nothing."""
+    _need_gpu()
+    import torch
+    cfg = D.RxConfig(payloadsz=8958, mode=D.MODE_WAVEFORM, flags=D.F_CSUM)
+    if broken:
+        r, fd = os.pipe()
+        os.close(r)
+    else:
+        fd = os.open(tmp_path / "raw.bin", os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        q = D.RxQueue(0, cfg, 8192)
+        q.set_raw_fd(fd, deferred=True)
+        for b in range(2):  # ~70 MB of raw stream per batch: the D2H takes milliseconds
+            umem, desc = D.synth_umem(8192, 9000, 9216, queue=b)
+            try:
+                q.process_batch(umem, desc)
+            except D.DqdkError:
+                assert broken and b == 1  # batch 0's deferred write() into the broken pipe
+            q.unregister_umem(umem)
+        q.close()  # batch 1's copy may still be in flight here
+    finally:
+        os.close(fd)
+    # the next queue's first batch, on fresh allocations
+    hcfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
+    umem, desc = D.synth_umem(4096, 1500, 4096, queue=7, faulty=True)
+    from test_gpu_parity import compare
+    compare(umem, desc, hcfg, check_hist=True, records=False)
+    torch.cuda.synchronize()

@@ -185,3 +185,58 @@ def test_slice_pass_over_a_full_stage_of_batches():
     otable *= k
     ocnt = {kk: (v if kk == "first_abort_idx" else k * v) for kk, v in ocnt.items()}
     assert_same(res, cnt, table, ores, ocnt, otable)
+
+
+def test_staging_probe_switches_piece_buffers_exactly():
+    """The staging placement probe (include/dqdk_gpu.h): a queue's first six
+    fused batches of >= 64K frames run on three candidate piece buffers in
+    turn (the decode's pieces and its overflow regions live there), the
+    seventh on the fastest, the others freed.  Faulty, peaked frames (pieces
+    and overflow regions both used) over nine batches: the table, results and
+    counters are nine times the oracle's, and the probe has decided."""
+    _need_gpu()
+    n = 1 << 16
+    umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, peaked=True, threads=HOST_THREADS)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
+    dev = torch.device("cuda:0")
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_res = torch.full((n * 8,), 0xEE, dtype=torch.uint8, device=dev)
+    k = 9
+    with D.RxQueue(0, cfg, n) as q:
+        q.set_stream(torch.cuda.current_stream().cuda_stream)
+        for b in range(k):
+            q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+            if b == 3:
+                assert q.staging_probe()["chosen"] == -1  # still probing
+        q.flush_histogram()
+        torch.cuda.synchronize()
+        probe = q.staging_probe()
+        cnt = q.counters()
+        table = q.histogram()
+    res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
+    assert probe["chosen"] in (0, 1, 2) and all(t > 0 for t in probe["ns_per_frame"]), probe
+    ores, ocnt, otable = oracle_full(umem, desc, cfg)
+    otable *= k
+    ocnt = {kk: (v if kk == "first_abort_idx" else k * v) for kk, v in ocnt.items()}
+    assert_same(res, cnt, table, ores, ocnt, otable)
+
+
+def test_staging_probe_off_and_below_its_batch_size(monkeypatch):
+    """DQDK_GPU_STAGING_PROBE=0 at queue creation, or batches under 64K
+    frames: no probe (chosen stays -1, nothing timed)."""
+    _need_gpu()
+    for env, n in (("0", 1 << 16), ("1", 4096)):
+        monkeypatch.setenv("DQDK_GPU_STAGING_PROBE", env)
+        umem, desc = D.synth_umem(n, 1500, 4096, threads=HOST_THREADS)
+        dev = torch.device("cuda:0")
+        d_umem = torch.from_numpy(umem).to(dev)
+        d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+        d_res = torch.empty((n * 8,), dtype=torch.uint8, device=dev)
+        with D.RxQueue(0, D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_PARTITIONED), n) as q:
+            q.set_stream(torch.cuda.current_stream().cuda_stream)
+            for _ in range(8):
+                q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), None)
+            torch.cuda.synchronize()
+            p = q.staging_probe()
+        assert p["chosen"] == -1 and not any(p["ns_per_frame"]), (env, n, p)
