@@ -65,6 +65,12 @@ dqdk_gpu_fp_cfg_t g_cfg{};
 std::vector<std::unique_ptr<FpWorker>> g_workers;
 uint32_t g_rr = 0;                    // round-robin device cursor
 std::atomic<uint64_t> g_gen{1};       // bumped by fini: invalidates thread caches
+// test hook (DQDK_GPU_FP_PEER_MERGE=1 at fp_init): fini's CSV merge takes the
+// cross-device branch (table copied on the worker's GPU, hipMemcpyPeer, add)
+// for every worker, a worker on w0's own GPU included (a peer copy within one
+// device is legal), so a one-GPU box exercises that branch's allocation,
+// copy and free ordering
+bool g_peer_merge = false;
 
 struct Cache {
     const void* key = nullptr;
@@ -243,6 +249,8 @@ int dqdk_gpu_fp_init(const dqdk_gpu_fp_cfg_t* cfg)
         return dqdk::set_error(-ENODEV, "fp_init: no such HIP device range");
     g_cfg = c;
     g_rr = 0;
+    const char* pm = getenv("DQDK_GPU_FP_PEER_MERGE");
+    g_peer_merge = pm && !strcmp(pm, "1");
     g_init = true;
     return 0;
 }
@@ -369,7 +377,7 @@ int dqdk_gpu_fp_fini(uint32_t* host_hist, int csv_fd, dqdk_gpu_counters_t* total
                         break;
                     }
                 }
-                if (w->device == w0->device) {
+                if (w->device == w0->device && !g_peer_merge) {
                     if (!(rc = dqdk_gpu_histogram_copy(w->q, tmp)))
                         rc = dqdk_gpu_queue_sync(w->q);
                 } else {  // another GPU: its table copied there, then peer-copied over

@@ -87,20 +87,39 @@ def merge_queue_histogram(q, dst: int = 0, group=None, buf: torch.Tensor | None 
     return buf
 
 
-def fini(q, runtime_ns: int, directory: str, histo_path: str | None = None, dst: int = 0, group=None) -> str | None:
-    """tristan_fini across ranks (src/tristan.c:162-233): merged counters,
-    merged histogram, the controller JSON line and the histogram CSV on `dst`.
-    Returns the JSON line on `dst`, None elsewhere."""
-    from .rx import tristan_summary
+def merge_queue_histogram_host(q, dst: int = 0, group=None) -> None:
+    """merge_queue_histogram for a host-side process group (gloo): the table
+    goes through host memory (``q.histogram()``), is SUM-reduced as an int32
+    CPU tensor, and ``dst``'s queue takes the job-wide table back
+    (``q.load_histogram``)."""
+    import numpy as np
 
-    dev = torch.device("cuda", q.device)
+    t = torch.from_numpy(q.histogram().view(np.int32))
+    reduce_histogram(t, dst=dst, group=group)
+    if dist.get_rank(group) == dst:
+        q.load_histogram(t.numpy().view(np.uint32))
+
+
+def fini(q, runtime_ns: int, directory: str, histo_path: str | None = None, dst: int = 0, group=None) -> str | None:
+    """tristan_fini across ranks (src/tristan.c:162-233): merged counters
+    (sum; first_abort_idx max), the longest runtime, the merged histogram,
+    the controller JSON line and the histogram CSV on `dst`.  Returns the
+    JSON line on `dst`, None elsewhere.  The reductions run where the group's
+    backend does: on the queue's GPU over RCCL (``nccl``), in host memory
+    over ``gloo``."""
+    from .rx import histo_enabled, tristan_summary
+
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", q.device) if on_gpu else torch.device("cpu")
     total = reduce_counters(q.counters(), device=dev, group=group)
     rt = torch.tensor([runtime_ns], dtype=torch.int64, device=dev)
     dist.all_reduce(rt, op=dist.ReduceOp.MAX, group=group)
-    from .rx import histo_enabled
     has_histo = histo_enabled(q.cfg.mode, q.cfg.flags)  # is_store_histo (no table materialised)
     if has_histo:
-        merge_queue_histogram(q, dst=dst, group=group)
+        if on_gpu:
+            merge_queue_histogram(q, dst=dst, group=group)
+        else:
+            merge_queue_histogram_host(q, dst=dst, group=group)
     if dist.get_rank(group) != dst:
         return None
     if has_histo and histo_path:

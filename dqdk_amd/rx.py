@@ -180,6 +180,18 @@ class RxQueue:
         L.check(L.lib().dqdk_gpu_histogram_get(self._h, out.ctypes.data), "histogram_get")
         return out
 
+    def load_histogram(self, table: np.ndarray) -> None:
+        """Replace the queue's table with a host u32 table (reset, then add a
+        device copy of it): dqdk_amd.multi's host-side merge."""
+        import torch
+
+        assert table.dtype == np.uint32 and table.size == L.HISTO_ENTRIES
+        buf = torch.from_numpy(np.ascontiguousarray(table).view(np.int32)).to(torch.device("cuda", self.device))
+        self.reset_histogram()
+        self.histogram_add(buf.data_ptr())
+        self.sync()
+        del buf
+
     def accumulate_histogram(self, into: np.ndarray) -> None:
         assert into.dtype == np.uint32 and into.size == L.HISTO_ENTRIES and into.flags.c_contiguous
         L.check(L.lib().dqdk_gpu_histogram_accumulate(self._h, into.ctypes.data), "histogram_accumulate")
