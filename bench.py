@@ -240,7 +240,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
 
     # correctness guard on the measured batch (cheap, outside the timed region)
     cnt = q.counters()
-    expect_pkts = n * (args.warmup + args.steps)
+    expect_pkts = n * (args.warmup + warm_extra + args.steps)
     assert cnt["rcvd_pkts"] == expect_pkts, cnt
     res = d_res.cpu().numpy().view(D.RESULT_DTYPE)
     assert (res["status"] == D.RX_OK).all(), np.bincount(res["status"])

@@ -2,7 +2,7 @@
 # Round 5, call c: the -m gpu suite on HEAD (staging probe, raw drain,
 # destroy-ordering test), the default bench line (with the probe's outcome),
 # SURVEY 8(d)'s packed-stride 1500 B line (stride 1536), the counter list of
-# this rocprofv3, and one SQ pass over the default 1500 B run (wave-cycle
+# this rocprofv3, one SQ pass over the default 1500 B run (wave-cycle
 # split of the decode: parked / issue-stalled / active, SALU / VALU / LDS / VMEM).
 # usage (on the GPU box): bash tools/r05/gpu_r05c.sh <tag>
 set -e
@@ -19,3 +19,7 @@ timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
     SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD -d gpurun_out/pmc_sq_${tag}_1500 -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-9000 --no-box-state \
     > gpurun_out/pmc_sq_${tag}_1500.log 2>&1
+# rx_part2 with contiguous item shares per block (piece starts staged once
+# per bucket): p2ct = the working tree, p2pf = HEAD (the phase-early loads)
+bash tools/ab_run.sh ${tag}_1500 "--no-9000 --no-box-state" p2pf p2ct
+bash tools/ab_run.sh ${tag}_9000 "--frame-len 9000 --no-9000 --no-box-state" p2pf p2ct
