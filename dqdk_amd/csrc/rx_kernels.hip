@@ -1291,60 +1291,90 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
 // cursor `cur`, in keys).  A round flushes whole triples (lines policy: whole
 // 128-B lines of 48 keys) and carries the rest to the next round; the last
 // flush writes everything, its last triple padded (the piece size marks the
-// valid keys).  All LDS reads of a few buckets are issued before their
-// stores, and every store is issued (its offset dropped past the run): no
-// dependent chain per bucket and a fixed VMEM pattern.  Rare: keys past a
-// full piece go to the block's overflow region (u32 keys, slot from an LDS
-// counter).
-template <bool kLines>
+// valid keys).  The buckets are written two at a time: lanes 0-31 take the
+// runs of bucket slot 2p, lanes 32-63 those of slot 2p + 1, one triple per
+// lane (a round's run is at most 44 triples, at most 32 in the lines policy;
+// longer ones take a second, rare pass), through one buffer descriptor per
+// pair with per-lane offsets -- half the store instructions and a third of
+// the address arithmetic of a bucket per instruction (timing-only builds put
+// the flush at 0.1 of the 1500 B decode and 0.25 of the 9000 B one, r05f).
+// All LDS reads of a few pairs are issued before their stores, and every
+// store is issued (its offset dropped past the run): a fixed VMEM pattern.
+// Rare: keys past a full piece go to the block's overflow region (u32 keys,
+// slot from an LDS counter).
+template <bool kLines, bool kLast>
 __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int lane, uint32_t wave, uint32_t& cur,
-                                            __amdgpu_buffer_rsrc_t ovf_rsrc, bool last)
+                                            __amdgpu_buffer_rsrc_t ovf_rsrc)
 {
+    constexpr bool last = kLast;
     const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
     uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
         c = min(lds.scnt[b] / kCntUnit, (uint32_t)kFCap);
         // lines policy: whole 128-B lines of triples (the piece cursor stays
         // line-aligned, so no store writes part of a line); else whole triples
-#ifndef DQDK_FLUSH_UNIT
-#define DQDK_FLUSH_UNIT kLineKeys
-#endif
-        w = last ? c : kLines ? c - c % (uint32_t)(DQDK_FLUSH_UNIT) : c - c % 3u;
+        w = last ? c : kLines ? c - c % kLineKeys : c - c % 3u;
         fit = min(w, a.piece_cap - cur);  // (cap and cur are multiples of 3: so is fit before the last flush)
     }
-    const uint32_t base = cur;
+    // the lane's bucket: byte offset of its next triple inside the bucket's
+    // region (cur is a multiple of 3 before the last flush's padded triple)
+    const uint32_t cbo = blockIdx.x * a.piece_words * 4u + (cur / 3u) * 8u;
     cur += fit;
-    constexpr int NJ = (kL1Buckets + kFWaves - 1) / kFWaves;
-#ifndef DQDK_FLUSH_G
-#define DQDK_FLUSH_G 6
-#endif
-    constexpr int G = DQDK_FLUSH_G;  // buckets per batch of reads (VGPRs: the load ring stays live)
-    uint32_t* const piece0 = a.part1 + (uint64_t)blockIdx.x * a.piece_words;
-#pragma unroll 1
-    for (int h = 0; h < (NJ + G - 1) / G; h++) {
-        uint32_t v[G][3];
+    constexpr int NJ = (kL1Buckets + kFWaves - 1) / kFWaves;  // 18 bucket slots per wave
+    constexpr int NP = (NJ + 1) / 2;                            // 9 pairs
+    constexpr int GP = 3;                                       // pairs per batch of LDS reads
+    const uint32_t half = (uint32_t)lane >> 5, t = (uint32_t)lane & 31u;
+    const uint32_t hoff = half * (uint32_t)kFWaves * (uint32_t)a.region * 4u;  // slot 2p + 1's bucket: 16 regions on
+    const uint64_t pair_bytes = (uint64_t)(kFWaves + 1) * a.region * 4u;
+    // pair p, triples [t0, t0 + 32) of each run: LDS reads (v) / pack + store
+    auto rd = [&](int p, uint32_t t0, uint32_t (&v)[3]) {
+        const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(2 * p) + (half ? (uint32_t)kFWaves : 0u),
+                                (uint32_t)kL1Buckets - 1);
 #pragma unroll
-        for (int q = 0; q < G; q++) {
-            const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(h * G + q), (uint32_t)kL1Buckets - 1);
-#pragma unroll
-            for (int i = 0; i < 3; i++)  // (lanes past the run read the next bucket's stage or the sink: unused)
-                v[q][i] = lds.stage[bj * kFCap + 3 * lane + i];
+        for (int i = 0; i < 3; i++)  // (lanes past the run read the next bucket's stage or the slack: unused)
+            v[i] = lds.stage[bj * kFCap + 3u * (t0 + t) + (uint32_t)i];
+    };
+    auto st = [&](int p, uint32_t t0, const uint32_t (&v)[3]) {
+        const uint32_t f0 = rdl(fit, 2 * p), f1 = 2 * p + 1 < NJ ? rdl(fit, 2 * p + 1) : 0u;
+        if ((f0 | f1) == 0 || 3u * t0 >= max(f0, f1))
+            return;  // (wave-uniform)
+        const uint32_t c0 = rdl(cbo, 2 * p), c1 = 2 * p + 1 < NJ ? rdl(cbo, 2 * p + 1) : 0u;
+        const uint32_t fj = half ? f1 : f0, cj = half ? c1 : c0;
+        const uint32_t tt = t0 + t;
+        const uint32_t bj0 = wave + (uint32_t)kFWaves * (uint32_t)(2 * p);
+        const __amdgpu_buffer_rsrc_t prs = uniform_rsrc(a.part1 + (uint64_t)bj0 * a.region, pair_bytes);
+        uint32_t k1 = v[1] & kTripleMask, k2 = v[2] & kTripleMask;
+        if (last) {  // the last flush's last triple: its slots past the run hold 0
+            k1 = 3u * tt + 1u < fj ? k1 : 0u;
+            k2 = 3u * tt + 2u < fj ? k2 : 0u;
         }
+        const u32x2 tr = {(v[0] & kTripleMask) | (k1 << kL1Shift), (k1 >> (32 - kL1Shift)) | (k2 << (2 * kL1Shift - 32))};
+        __builtin_amdgcn_raw_buffer_store_b64(tr, prs, 3u * tt < fj ? hoff + cj + tt * 8u : kOOB, 0, DQDK_FST_AUX);
+    };
+#pragma unroll 1
+    for (int h = 0; h < NP; h += GP) {
+        uint32_t v[GP][3];
 #pragma unroll
-        for (int q = 0; q < G; q++) {
-            const int j = h * G + q;
-            if (j < NJ) {
-                const uint32_t bj = wave + (uint32_t)kFWaves * (uint32_t)j;
-                const uint32_t fj = rdl(fit, j), bsj = rdl(base, j);
-                const __amdgpu_buffer_rsrc_t prs =
-                    uniform_rsrc(piece0 + (uint64_t)min(bj, (uint32_t)kL1Buckets - 1) * a.region, a.piece_words * 4u);
-                // the last flush's last triple: its slots past the run hold 0
-                const uint32_t k0 = v[q][0] & kTripleMask;
-                const uint32_t k1 = 3u * lane + 1u < fj ? v[q][1] & kTripleMask : 0u;
-                const uint32_t k2 = 3u * lane + 2u < fj ? v[q][2] & kTripleMask : 0u;
-                const u32x2 t = {k0 | (k1 << kL1Shift), (k1 >> (32 - kL1Shift)) | (k2 << (2 * kL1Shift - 32))};
-                const uint32_t o = (bsj / 3u + (uint32_t)lane) * 8u;
-                __builtin_amdgcn_raw_buffer_store_b64(t, prs, 3u * lane < fj ? o : kOOB, 0, DQDK_FST_AUX);
+        for (int q = 0; q < GP; q++)
+            if (h + q < NP)
+                rd(h + q, 0u, v[q]);
+#pragma unroll
+        for (int q = 0; q < GP; q++)
+            if (h + q < NP)
+                st(h + q, 0u, v[q]);
+    }
+    // runs past 32 triples (96 keys; in the lines policy only at the last
+    // flush: its rounds flush at most two 48-key lines of a bucket)
+    if (!kLines || kLast) {
+        uint64_t m = __ballot(fit > 96u);
+        while (m) {
+            const int p = (int)__builtin_ctzll(m) >> 1;
+            m &= ~(3ull << (2 * p));  // (both slots of the pair at once)
+            const uint32_t fmax = max(rdl(fit, 2 * p), 2 * p + 1 < NJ ? rdl(fit, 2 * p + 1) : 0u);
+            for (uint32_t t0 = 32; 3u * t0 < fmax; t0 += 32) {
+                uint32_t v[3];
+                rd(p, t0, v);
+                st(p, t0, v);
             }
         }
     }
@@ -1552,7 +1582,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             }
             if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
                 lds_barrier();
-                fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, false);
+                fused_flush<kLines, false>(a, lds, lane, wave, fcur, ovf_rsrc);
                 lds_barrier();
             }
         }
@@ -1575,7 +1605,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
     // the keys still staged, then the piece sizes for rx_part1 / rx_part2
     lds_barrier();
-    fused_flush<kLines>(a, lds, lane, wave, fcur, ovf_rsrc, true);
+    fused_flush<kLines, true>(a, lds, lane, wave, fcur, ovf_rsrc);
     {
         const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
         if (b < (uint32_t)kL1Buckets)
