@@ -535,8 +535,18 @@ int clean_slot(dqdk_gpu_queue* q, uint32_t* slot_scratch)
 {
     if (q->slot_dirty.size() < q->hist_k)
         q->slot_dirty.resize(q->hist_k, 1);
-    if (q->slot_dirty[q->hist_pending] || q->p2zero_off)
+    if (q->slot_dirty[q->hist_pending] || q->p2zero_off) {
         HIPCHK(hipMemsetAsync(slot_scratch, 0, kZeroWords * sizeof(uint32_t), q->stream));
+        // a batch that failed on the way may have left a last-block ticket
+        // raised (rx_count's, the fused decode's, rx_part2's): zero between
+        // launches, else no block would ever be the last (advisor r4)
+        static_assert(kFoldTicketWord == kTicketWord + 1 && kPart2TicketWord == kTicketWord + 2, "ticket words");
+        HIPCHK(hipMemsetAsync(q->d_batch + kTicketWord, 0, 3 * sizeof(uint64_t), q->stream));
+        // and the folded counters' accumulators: zero, the first-failure
+        // word (FoldWord F_FAIL = 9) all ones, as at creation
+        HIPCHK(hipMemsetAsync(q->d_blkcnt, 0, kFoldWords * sizeof(uint64_t), q->stream));
+        HIPCHK(hipMemsetAsync((uint64_t*)q->d_blkcnt + 9, 0xff, sizeof(uint64_t), q->stream));
+    }
     q->slot_dirty[q->hist_pending] = 1;
     return 0;
 }
