@@ -126,13 +126,7 @@ constexpr int kFWaves = 16;
 constexpr int kFThreads = kFWaves * 64;
 // The frame's checksum tail is corrected in the window loop (no 16-KB
 // per-frame tail copy in LDS): that room goes to the bucket stages.
-#ifndef DQDK_INLINE_TAIL
-#define DQDK_INLINE_TAIL 1
-#endif
-#ifndef DQDK_FCAP
-#define DQDK_FCAP (DQDK_INLINE_TAIL ? 134 : 120)
-#endif
-constexpr int kFCap = DQDK_FCAP;
+constexpr int kFCap = 134;
 constexpr uint32_t kTripleMask = (1u << kL1Shift) - 1;  // a bucket-local key
 constexpr uint32_t kLineKeys = 48;                     // keys of one 128-B line of triples
 struct FusedGeom {

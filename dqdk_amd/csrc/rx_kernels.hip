@@ -984,9 +984,6 @@ struct FusedLds {
     uint32_t scnt[kL1Buckets + 4];   // staged keys per bucket this round (returning LDS atomics)
     uint32_t sum[kFWaves * 64];      // checksum word sums per frame
     uint32_t oob[kFWaves * 64];      // out-of-bounds events per frame
-#if !DQDK_INLINE_TAIL
-    u32x4 tail[kFWaves * 64];        // last checksum chunk per frame
-#endif
     uint32_t wtot[kFWaves];          // windows of each wave's tile
     uint32_t ovf_n;                  // keys in this block's private overflow region
     alignas(8) uint32_t fc[kFoldWords];  // folded counters of the block (FoldWord; the bytes word pair is a u64)
@@ -1121,54 +1118,6 @@ __device__ __forceinline__ void ovf_put(const RxArgs& a, __amdgpu_buffer_rsrc_t 
         __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One event per 16-B chunk (as decode_chunk): the key goes to the LDS stage
-// of its bucket; past kFCap staged keys (rare) it goes to the block's private
-// overflow region.  The overflow store is issued by every lane of every
-// window (dropped out of range unless the key overflows) and its slot comes
-// from an LDS counter: the window loop's VMEM pattern stays fixed, so the
-// compiler waits for ring loads with vmcnt(N) instead of draining the ring (a
-// conditional global atomic or store here would force near-full waits).
-__device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uint32_t r, uint32_t e, uint32_t Ef,
-                                            uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc)
-{
-    const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);  // event bytes 2..5
-    const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);  // event bytes 6..9
-    const uint32_t ch = x & 0xffffu;
-    const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);   // event bytes 5,6 = energy >> 8
-    const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);             // hist_class:3
-    const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;  // ((ch*6 + hc) << 16) | bin
-    const bool inb = ch < kChannels && hc < kHists;                  // histogram_event's bounds (tristan.c:236-241)
-    // one returning LDS add per event, to the bucket's stage count or to the
-    // frame's out-of-bounds count, and one masked stage store: two masked
-    // operations instead of two levels of divergent branches (decode -2 % at
-    // 1500 B, A/B on one box; the same at 9000 B)
-    const bool has = e < Ef;
-    const uint32_t b = key >> kL1Shift;
-    uint32_t* const cnt = inb ? &lds.scnt[min(b, (uint32_t)kL1Buckets - 1)] : &lds.oob[oob_slot];
-    uint32_t slot = 0;
-    if (has)
-        slot = atomicAdd(cnt, 1u);
-    const bool ink = has && inb;
-    if (ink && slot < (uint32_t)kFCap)
-        lds.stage[b * kFCap + slot] = key;
-    const bool ov = ink && slot >= (uint32_t)kFCap;
-
-    // overflow slots: one LDS atomic per wave (lanes ranked by mbcnt), not one
-    // per key on the block's single counter (64 lanes on one address serialise)
-    const uint64_t om = __ballot(ov);
-    if (om) {
-        const uint32_t first = (uint32_t)__builtin_ctzll(om);
-        uint32_t base = 0;
-        if ((uint32_t)(threadIdx.x & 63) == first)
-            base = atomicAdd(&lds.ovf_n, (uint32_t)__builtin_popcountll(om));
-        base = rdl(base, first);
-        ovf_put(a, ovf_rsrc, key, ov,
-                base + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u)));
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32(key, ovf_rsrc, kOOB, 0, 0);
-    }
-}
-
 // Both chunks of a window at once, without divergent branches: every lane
 // issues two returning LDS adds (an event's bucket stage count, a frame's
 // out-of-bounds count, or -- lanes without an event -- a private sink word of
@@ -1177,12 +1126,6 @@ __device__ __forceinline__ void fused_chunk(const RxArgs& a, const u32x4& v, uin
 // instead of once per chunk, and no exec mask is saved or restored.  Keys
 // past kFCap (rare) go to the block's overflow region behind one
 // wave-uniform branch.
-#ifndef DQDK_FPAIR
-#define DQDK_FPAIR 1
-#endif
-// Stage counts (and per-frame out-of-bounds counts) step by kCntUnit: with 4
-// a count is the byte offset of the slot, so a stage address is one mad.
-constexpr uint32_t kCntUnit = DQDK_FPAIR >= 2 ? 4u : 1u;
 __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0,
                                            uint32_t Ef, uint32_t oob_slot, FusedLds& lds,
                                            __amdgpu_buffer_rsrc_t ovf_rsrc, uint32_t lane)
@@ -1208,18 +1151,6 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
         ink[c] = has && inb;
         cnt[c] = has ? (inb ? &lds.scnt[b[c]] : &lds.oob[oob_slot]) : sink;
     }
-#if DQDK_FPAIR >= 2
-    // counts in bytes: the slot's stage address is b * (4 kFCap) + count
-    const uint32_t s0 = atomicAdd(cnt[0], kCntUnit);
-    const uint32_t s1 = atomicAdd(cnt[1], kCntUnit);
-    const bool st0 = ink[0] && s0 < 4u * kFCap, st1 = ink[1] && s1 < 4u * kFCap;
-    uint8_t* const stage8 = (uint8_t*)lds.stage;
-    *(uint32_t*)(st0 ? stage8 + __umul24(b[0], 4u * kFCap) + s0 : (uint8_t*)sink) = key[0];
-    *(uint32_t*)(st1 ? stage8 + __umul24(b[1], 4u * kFCap) + s1 : (uint8_t*)sink) = key[1];
-    const bool ov0 = ink[0] && s0 >= 4u * kFCap, ov1 = ink[1] && s1 >= 4u * kFCap;
-    if (__builtin_amdgcn_ballot_w64(ov0 || ov1)) {  // rare: overflow slots, one LDS atomic per wave
-        const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
-#else
     const uint32_t s0 = atomicAdd(cnt[0], 1u);
     const uint32_t s1 = atomicAdd(cnt[1], 1u);
     const bool st0 = ink[0] && s0 < (uint32_t)kFCap, st1 = ink[1] && s1 < (uint32_t)kFCap;
@@ -1228,7 +1159,6 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     const bool ov0 = ink[0] && s0 >= (uint32_t)kFCap, ov1 = ink[1] && s1 >= (uint32_t)kFCap;
     const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
     if (m0 | m1) {  // rare: overflow slots, one LDS atomic per wave
-#endif
         const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
         const uint32_t first = (uint32_t)__builtin_ctzll(m0 | m1);
         uint32_t base = 0;
@@ -1256,21 +1186,21 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
     for (int k = 0; k < kAEv; k++) {
         const bool has = (uint32_t)k < na, inb = akey[k] != DQDK_KEY_NONE;
         const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
-        sl[k] = atomicAdd(has ? (inb ? &lds.scnt[b] : &lds.oob[oob_slot]) : sink, kCntUnit);
+        sl[k] = atomicAdd(has ? (inb ? &lds.scnt[b] : &lds.oob[oob_slot]) : sink, 1u);
     }
     bool anyov = false;
 #pragma unroll
     for (int k = 0; k < kAEv; k++) {
         const bool ink = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE;
         const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
-        const bool st = ink && sl[k] < kCntUnit * kFCap;
-        *(st ? &lds.stage[b * kFCap + sl[k] / kCntUnit] : sink) = akey[k];
+        const bool st = ink && sl[k] < (uint32_t)kFCap;
+        *(st ? &lds.stage[b * kFCap + sl[k]] : sink) = akey[k];
         anyov |= ink && !st;
     }
     if (__ballot(anyov)) {  // rare: overflow slots
 #pragma unroll
         for (int k = 0; k < kAEv; k++) {
-            const bool ov = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE && sl[k] >= kCntUnit * kFCap;
+            const bool ov = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE && sl[k] >= (uint32_t)kFCap;
             const uint64_t om = __ballot(ov);
             if (om) {
                 const uint32_t first = (uint32_t)__builtin_ctzll(om);
@@ -1310,7 +1240,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
     const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
     uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
-        c = min(lds.scnt[b] / kCntUnit, (uint32_t)kFCap);
+        c = min(lds.scnt[b], (uint32_t)kFCap);
         // lines policy: whole 128-B lines of triples (the piece cursor stays
         // line-aligned, so no store writes part of a line); else whole triples
         w = last ? c : kLines ? c - c % kLineKeys : c - c % 3u;
@@ -1409,7 +1339,7 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
             lds.stage[b * kFCap + 1] = x1;
     }
     if (b < (uint32_t)kL1Buckets)
-        lds.scnt[b] = (c - w) * kCntUnit;
+        lds.scnt[b] = c - w;
 }
 
 // Two policies for the pieces' partial lines (runs end mid-line), chosen by
@@ -1545,7 +1475,6 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                     csum_pair(b0[d], b1[d], u16x2{1, 1}, u16x2{1, 1}, acc0, acc1);
                 }
                 if (active && wp == P.tw) {  // (wave-uniform) the frame's last checksum chunk
-#if DQDK_INLINE_TAIL
                     // its bytes past the datagram leave the sum here, by the
                     // lane holding it (no per-frame LDS copy for phase C)
                     if (lane == (int)P.tl) {
@@ -1554,19 +1483,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                         else
                             acc0 -= tail_corr(b0[d], (int)P.keep);
                     }
-#else
-                    if (lane == (int)P.tl)
-                        lds.tail[wslot0 + jp] = P.th ? b1[d] : b0[d];
-#endif
                 }
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
-#if DQDK_FPAIR
                 fused_pair(a, b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
-#else
-                fused_chunk(a, b0[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc);
-                fused_chunk(a, b1[d], P.r, e0 + 64u, Ef, wslot0 + jp, lds, ovf_rsrc);
-#endif
                 if (active && ++wp == P.nwin) {
                     frame_sum_add(&lds.sum[wslot0 + jp], &lds.stage[kL1Buckets * kFCap + lane], acc0 + acc1,
                                   (lane & 15) == 15);
@@ -1589,14 +1509,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 
         // ---- phase C ----
         const uint32_t my = wslot0 + (uint32_t)lane;
-        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my] / kCntUnit;
+        const uint32_t sum_t = lds.sum[my], sum_oob = lds.oob[my];
         lds.sum[my] = 0;
         lds.oob[my] = 0;
-#if DQDK_INLINE_TAIL
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, u32x4{0u, 0u, 0u, 0u});
-#else
-        phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
-#endif
         if (a.fold)
             fold_frames(a, lds, live, r, i, lane);
         // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
