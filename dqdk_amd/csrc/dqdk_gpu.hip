@@ -366,11 +366,11 @@ int hist_flush(dqdk_gpu_queue* q)
 }
 
 // Windows per wave per fused round: the block's 16 waves stage at most
-// 16 * W * min(E, 128) keys per round into 284 * kFCap slots (kFCap 134).
-// Measured (A/B, one box each): W = 16 at 1500 B (~61 % mean fill; 12 and 20
-// windows lost 1 % and 5-7 %), W = 12 at 9000 B, where the lines policy
-// carries up to 47 keys per bucket between rounds (16 windows overflowed
-// three times as many keys to rx_part1; 8 cost the decode more).
+// 16 * W * min(E, 128) keys per round into 284 * kFCap slots (kFCap 198,
+// keys packed three to a word).  Measured (A/B, r05l/r05m): W = 28 at 1500 B
+// (fill 70 %; 24 and 32 windows slower, 32 overflowing more keys), W = 16 at
+// 9000 B, where the lines policy carries up to 47 keys per bucket between
+// rounds (20 windows overflowed three times as many keys to rx_part1).
 //
 // The pieces' runs end mid-line.  Below 128 events per frame (1500 B) the
 // frame loads are non-temporal and the partial lines complete in L2; from
@@ -652,8 +652,8 @@ int read_knobs(dqdk_gpu_queue* q)
                                         " is an A/B variant (build with -DDQDK_AB_VARIANTS)").c_str());
         q->fused_pol = p;
     }
-#ifndef DQDK_FUSED_FILL  // stage fill target, percent (134-key stage: W = 16 at 1500 B, 12 at 9000 B; r04g: 20 / 16 slower)
-#define DQDK_FUSED_FILL (q->E >= 128 ? 65 : 61)
+#ifndef DQDK_FUSED_FILL  // stage fill target, percent (198-key stage: W = 28 at 1500 B, 16 at 9000 B; r05l)
+#define DQDK_FUSED_FILL (q->E >= 128 ? 65 : 70)
 #endif
     double fill = DQDK_FUSED_FILL;
     if (const char* v = env("DQDK_GPU_FUSED_FILL"))

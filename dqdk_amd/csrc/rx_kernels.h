@@ -125,8 +125,11 @@ constexpr int kItemOffs = kSubs + 1;  // u16 run offsets per part2 item (one chu
 constexpr int kFWaves = 16;
 constexpr int kFThreads = kFWaves * 64;
 // The frame's checksum tail is corrected in the window loop (no 16-KB
-// per-frame tail copy in LDS): that room goes to the bucket stages.
-constexpr int kFCap = 134;
+// per-frame tail copy in LDS): that room goes to the bucket stages, which
+// hold their keys packed as the pieces do (three to an 8-B word): kFCapW
+// words, kFCap keys per bucket.
+constexpr int kFCapW = 66;
+constexpr int kFCap = 3 * kFCapW;
 constexpr uint32_t kTripleMask = (1u << kL1Shift) - 1;  // a bucket-local key
 constexpr uint32_t kLineKeys = 48;                     // keys of one 128-B line of triples
 struct FusedGeom {

@@ -10,10 +10,13 @@ namespace dqdk {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // (a helper taking the dword by value: __builtin_bit_cast applied directly
 // to an ext_vector element such as v.y reads element 0 with hipcc 7.2)
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ u32x2 as_u32x2(uint64_t x) { return __builtin_bit_cast(u32x2, x); }
+__device__ __forceinline__ u32x4 as_u32x4(u64x2 x) { return __builtin_bit_cast(u32x4, x); }
 
 // Byte layout constants (src/tristan.h:55-60).
 constexpr uint32_t kChannels = DQDK_TRISTAN_CHANNELS;
@@ -979,8 +982,14 @@ __global__ void __launch_bounds__(kTile) fp_decode_kernel(PayloadArgs a)
 // there to the overflow list, which rx_part1 groups like frame-order records.
 // Frames decoded but later failing the UDP checksum are listed for rx_fixup.
 // ===========================================================================
+// The stage holds each bucket's keys as its piece will, three 21-bit
+// bucket-local keys to an 8-B word in slot order (k0 | k1 << 21 | k2 << 42):
+// a key is OR-ed into its field (the word is zero until then: a flushed word
+// is zeroed), and a flush copies whole words, unchanged, to the piece.
+constexpr uint32_t kStageWords = kL1Buckets * kFCapW;
 struct FusedLds {
-    uint32_t stage[kL1Buckets * kFCap + 96];  // (+96: the flush reads 192 slots per bucket; the lanes' sink words)
+    alignas(16) uint64_t stage[kStageWords + 64];  // (+64: the flush reads up to 128 words a bucket; the OR sinks)
+    uint32_t csink[64];              // the lanes' count sinks (no event)
     uint32_t scnt[kL1Buckets + 4];   // staged keys per bucket this round (returning LDS atomics)
     uint32_t sum[kFWaves * 64];      // checksum word sums per frame
     uint32_t oob[kFWaves * 64];      // out-of-bounds events per frame
@@ -1118,6 +1127,16 @@ __device__ __forceinline__ void ovf_put(const RxArgs& a, __amdgpu_buffer_rsrc_t 
         __hip_atomic_fetch_add(&a.hist[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A staged key into its field: slot s of bucket b is field s % 3 of word
+// s / 3 (s < kFCap); a lane without one ORs 0 into its sink word.
+__device__ __forceinline__ void stage_key(FusedLds& lds, bool st, uint32_t b, uint32_t s, uint32_t key, uint32_t lane)
+{
+    const uint32_t q = __umulhi(s, 0xaaaaaaabu) >> 1, f = s - 3u * q;
+    uint64_t* const wd = st ? &lds.stage[b * (uint32_t)kFCapW + q] : &lds.stage[kStageWords + (lane & 31u)];
+    const uint64_t v = st ? (uint64_t)(key & kTripleMask) << (kL1Shift * f) : 0ull;
+    __hip_atomic_fetch_or(wd, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Both chunks of a window at once, without divergent branches: every lane
 // issues two returning LDS adds (an event's bucket stage count, a frame's
 // out-of-bounds count, or -- lanes without an event -- a private sink word of
@@ -1133,9 +1152,7 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     uint32_t key[2], b[2];
     uint32_t* cnt[2];
     bool ink[2];
-    // the lane's sink: the 64 slack words after the last bucket's stage (read
-    // by the flush of bucket 283 only past its count, so never stored)
-    uint32_t* const sink = &lds.stage[kL1Buckets * kFCap + lane];
+    uint32_t* const sink = &lds.csink[lane];  // (the lane's count sink)
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         const u32x4& v = c ? vb : va;
@@ -1154,8 +1171,8 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     const uint32_t s0 = atomicAdd(cnt[0], 1u);
     const uint32_t s1 = atomicAdd(cnt[1], 1u);
     const bool st0 = ink[0] && s0 < (uint32_t)kFCap, st1 = ink[1] && s1 < (uint32_t)kFCap;
-    *(st0 ? &lds.stage[b[0] * kFCap + s0] : sink) = key[0];
-    *(st1 ? &lds.stage[b[1] * kFCap + s1] : sink) = key[1];
+    stage_key(lds, st0, b[0], s0, key[0], lane);
+    stage_key(lds, st1, b[1], s1, key[1], lane);
     const bool ov0 = ink[0] && s0 >= (uint32_t)kFCap, ov1 = ink[1] && s1 >= (uint32_t)kFCap;
     const uint64_t m0 = __ballot(ov0), m1 = __ballot(ov1);
     if (m0 | m1) {  // rare: overflow slots, one LDS atomic per wave
@@ -1180,7 +1197,7 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
                                              uint32_t oob_slot, FusedLds& lds, __amdgpu_buffer_rsrc_t ovf_rsrc,
                                              uint32_t lane)
 {
-    uint32_t* const sink = &lds.stage[kL1Buckets * kFCap + lane];
+    uint32_t* const sink = &lds.csink[lane];
     uint32_t sl[kAEv];
 #pragma unroll
     for (int k = 0; k < kAEv; k++) {
@@ -1194,7 +1211,7 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
         const bool ink = (uint32_t)k < na && akey[k] != DQDK_KEY_NONE;
         const uint32_t b = min(akey[k] >> kL1Shift, (uint32_t)kL1Buckets - 1);
         const bool st = ink && sl[k] < (uint32_t)kFCap;
-        *(st ? &lds.stage[b * kFCap + sl[k]] : sink) = akey[k];
+        stage_key(lds, st, b, sl[k], akey[k], lane);
         anyov |= ink && !st;
     }
     if (__ballot(anyov)) {  // rare: overflow slots
@@ -1216,22 +1233,23 @@ __device__ __forceinline__ void fused_keys_a(const RxArgs& a, const uint32_t (&a
     }
 }
 
-// Append the round's staged runs to the block's pieces as key triples.  Wave
-// w owns buckets w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece
-// cursor `cur`, in keys).  A round flushes whole triples (lines policy: whole
-// 128-B lines of 48 keys) and carries the rest to the next round; the last
-// flush writes everything, its last triple padded (the piece size marks the
-// valid keys).  The buckets are written two at a time: lanes 0-31 take the
-// runs of bucket slot 2p, lanes 32-63 those of slot 2p + 1, one triple per
-// lane (a round's run is at most 44 triples, at most 32 in the lines policy;
-// longer ones take a second, rare pass), through one buffer descriptor per
-// pair with per-lane offsets -- half the store instructions and a third of
-// the address arithmetic of a bucket per instruction (timing-only builds put
-// the flush at 0.1 of the 1500 B decode and 0.25 of the 9000 B one, r05f).
-// All LDS reads of a few pairs are issued before their stores, and every
-// store is issued (its offset dropped past the run): a fixed VMEM pattern.
-// Rare: keys past a full piece go to the block's overflow region (u32 keys,
-// slot from an LDS counter).
+// Append the round's staged runs to the block's pieces.  Wave w owns buckets
+// w, w + kFWaves, ... (lane j: bucket w + kFWaves*j, its piece cursor `cur`,
+// in keys).  The stage already holds the piece's format (three keys to a
+// word), so a run's words are copied unchanged.  A round flushes whole words
+// (lines policy: whole 128-B lines, 16 words) and carries the rest (at most
+// one word; lines policy: at most 16) to the stage's start; the last flush
+// writes everything (the fields past the run hold zero, or keys sent to the
+// overflow region: the piece size marks the valid keys).  The buckets are
+// written two at a time: lanes 0-31 take the words of bucket slot 2p, lanes
+// 32-63 those of slot 2p + 1, two words (one LDS read, one 16-B store) per
+// lane and an 8-B store for a run's odd last word -- runs of up to 64 words
+// in one pass, longer ones (a stage nearly full) in a second, rare pass --
+// through one buffer descriptor per pair with per-lane offsets.  Every store
+// is issued (its offset dropped past the run): a fixed VMEM pattern.  The
+// flushed words are zeroed for the next round's ORs.  Rare: keys past a full
+// piece go to the block's overflow region (u32 keys, slot from an LDS
+// counter).
 template <bool kLines, bool kLast>
 __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int lane, uint32_t wave, uint32_t& cur,
                                             __amdgpu_buffer_rsrc_t ovf_rsrc)
@@ -1241,105 +1259,122 @@ __device__ __forceinline__ void fused_flush(const RxArgs& a, FusedLds& lds, int 
     uint32_t c = 0, w = 0, fit = 0;
     if (b < (uint32_t)kL1Buckets) {
         c = min(lds.scnt[b], (uint32_t)kFCap);
-        // lines policy: whole 128-B lines of triples (the piece cursor stays
-        // line-aligned, so no store writes part of a line); else whole triples
+        // lines policy: whole 128-B lines of words (the piece cursor stays
+        // line-aligned, so no store writes part of a line); else whole words
         w = last ? c : kLines ? c - c % kLineKeys : c - c % 3u;
         fit = min(w, a.piece_cap - cur);  // (cap and cur are multiples of 3: so is fit before the last flush)
     }
-    // the lane's bucket: byte offset of its next triple inside the bucket's
-    // region (cur is a multiple of 3 before the last flush's padded triple)
+    const uint32_t nw = (fit + 2u) / 3u;           // words to the piece
+    const uint32_t nz = last ? 0u : w / 3u;         // words flushed (to the piece or the overflow): zeroed
+    // the lane's bucket: byte offset of its next word inside the bucket's
+    // region (cur is a multiple of 3 before the last flush)
     const uint32_t cbo = blockIdx.x * a.piece_words * 4u + (cur / 3u) * 8u;
-    cur += fit;
     constexpr int NJ = (kL1Buckets + kFWaves - 1) / kFWaves;  // 18 bucket slots per wave
-    constexpr int NP = (NJ + 1) / 2;                            // 9 pairs
-    constexpr int GP = 3;                                       // pairs per batch of LDS reads
+    constexpr int NP = (NJ + 1) / 2;                          // 9 pairs
+    constexpr int GP = 3;                                     // pairs per batch of LDS reads
     const uint32_t half = (uint32_t)lane >> 5, t = (uint32_t)lane & 31u;
     const uint32_t hoff = half * (uint32_t)kFWaves * (uint32_t)a.region * 4u;  // slot 2p + 1's bucket: 16 regions on
     const uint64_t pair_bytes = (uint64_t)(kFWaves + 1) * a.region * 4u;
-    // pair p, triples [t0, t0 + 32) of each run: LDS reads (v) / pack + store
-    auto rd = [&](int p, uint32_t t0, uint32_t (&v)[3]) {
-        const uint32_t bj = min(wave + (uint32_t)kFWaves * (uint32_t)(2 * p) + (half ? (uint32_t)kFWaves : 0u),
-                                (uint32_t)kL1Buckets - 1);
-#pragma unroll
-        for (int i = 0; i < 3; i++)  // (lanes past the run read the next bucket's stage or the slack: unused)
-            v[i] = lds.stage[bj * kFCap + 3u * (t0 + t) + (uint32_t)i];
-    };
-    auto st = [&](int p, uint32_t t0, const uint32_t (&v)[3]) {
-        const uint32_t f0 = rdl(fit, 2 * p), f1 = 2 * p + 1 < NJ ? rdl(fit, 2 * p + 1) : 0u;
-        if ((f0 | f1) == 0 || 3u * t0 >= max(f0, f1))
-            return;  // (wave-uniform)
-        const uint32_t c0 = rdl(cbo, 2 * p), c1 = 2 * p + 1 < NJ ? rdl(cbo, 2 * p + 1) : 0u;
-        const uint32_t fj = half ? f1 : f0, cj = half ? c1 : c0;
-        const uint32_t tt = t0 + t;
-        const uint32_t bj0 = wave + (uint32_t)kFWaves * (uint32_t)(2 * p);
-        const __amdgpu_buffer_rsrc_t prs = uniform_rsrc(a.part1 + (uint64_t)bj0 * a.region, pair_bytes);
-        uint32_t k1 = v[1] & kTripleMask, k2 = v[2] & kTripleMask;
-        if (last) {  // the last flush's last triple: its slots past the run hold 0
-            k1 = 3u * tt + 1u < fj ? k1 : 0u;
-            k2 = 3u * tt + 2u < fj ? k2 : 0u;
-        }
-        const u32x2 tr = {(v[0] & kTripleMask) | (k1 << kL1Shift), (k1 >> (32 - kL1Shift)) | (k2 << (2 * kL1Shift - 32))};
-        __builtin_amdgcn_raw_buffer_store_b64(tr, prs, 3u * tt < fj ? hoff + cj + tt * 8u : kOOB, 0, DQDK_FST_AUX);
-    };
-#pragma unroll 1
-    for (int h = 0; h < NP; h += GP) {
-        uint32_t v[GP][3];
-#pragma unroll
-        for (int q = 0; q < GP; q++)
-            if (h + q < NP)
-                rd(h + q, 0u, v[q]);
-#pragma unroll
-        for (int q = 0; q < GP; q++)
-            if (h + q < NP)
-                st(h + q, 0u, v[q]);
-    }
-    // runs past 32 triples (96 keys; in the lines policy only at the last
-    // flush: its rounds flush at most two 48-key lines of a bucket)
-    if (!kLines || kLast) {
-        uint64_t m = __ballot(fit > 96u);
-        while (m) {
-            const int p = (int)__builtin_ctzll(m) >> 1;
-            m &= ~(3ull << (2 * p));  // (both slots of the pair at once)
-            const uint32_t fmax = max(rdl(fit, 2 * p), 2 * p + 1 < NJ ? rdl(fit, 2 * p + 1) : 0u);
-            for (uint32_t t0 = 32; 3u * t0 < fmax; t0 += 32) {
-                uint32_t v[3];
-                rd(p, t0, v);
-                st(p, t0, v);
-            }
-        }
-    }
+    // rare: keys past a full piece (words [fit / 3, w / 3)) to the overflow
+    // region, before their words are zeroed
     for (uint64_t m = __ballot(fit < w); m; m &= m - 1) {
         const uint32_t j = (uint32_t)__builtin_ctzll(m);
         const uint32_t bj = wave + (uint32_t)kFWaves * j;
-        const uint32_t fj = rdl(fit, j), nov = rdl(w, j) - fj;
+        const uint32_t fj = rdl(fit, j), nov = rdl(w, j) - fj;  // (fj: a multiple of 3 unless last)
         uint32_t o = 0;
         if (lane == 0)
             o = atomicAdd(&lds.ovf_n, nov);
         o = rfl(o);
-        for (uint32_t t = (uint32_t)lane; t < nov; t += 64)
-            ovf_put(a, ovf_rsrc, lds.stage[bj * kFCap + fj + t], true, o + t);
-    }
-    // carry the remainders to the stage's start (fewer keys than were
-    // flushed, so source and destination do not overlap)
-    if (kLines) {  // up to 47 keys: a wave per bucket
-        for (uint64_t m = __ballot(w != 0 && c > w); m; m &= m - 1) {
-            const uint32_t j = (uint32_t)__builtin_ctzll(m);
-            const uint32_t bj = wave + (uint32_t)kFWaves * j;
-            const uint32_t wj = rdl(w, j), r = rdl(c, j) - wj;
-            uint32_t x = 0;
-            if ((uint32_t)lane < r)
-                x = lds.stage[bj * kFCap + wj + lane];
-            if ((uint32_t)lane < r)
-                lds.stage[bj * kFCap + lane] = x;
+        for (uint32_t k = (uint32_t)lane; k < nov; k += 64) {
+            const uint32_t s = fj + k, q = s / 3u;
+            const uint32_t key = (uint32_t)(lds.stage[bj * (uint32_t)kFCapW + q] >> (kL1Shift * (s - 3u * q))) & kTripleMask;
+            ovf_put(a, ovf_rsrc, (bj << kL1Shift) | key, true, o + k);
         }
-    } else if (w != 0 && c > w) {  // up to 2 keys: each lane its own bucket
-        const uint32_t x0 = lds.stage[b * kFCap + w], x1 = lds.stage[b * kFCap + w + 1];
-        lds.stage[b * kFCap] = x0;
-        if (c - w > 1)
-            lds.stage[b * kFCap + 1] = x1;
     }
-    if (b < (uint32_t)kL1Buckets)
+    const uint64_t anyf = __ballot(nw != 0 || nz != 0);
+    // pair p, words [2 t0, 2 t0 + 64) of each run: LDS reads (v) / stores + zeroing
+    auto rd = [&](int p, uint32_t t0, u64x2& v) {
+        const uint32_t bj = min(wave + (uint32_t)kFWaves * ((uint32_t)(2 * p) + half), (uint32_t)kL1Buckets - 1);
+        // (lanes past the run read the next bucket's words or the slack: unused)
+        v = *(const u64x2*)&lds.stage[bj * (uint32_t)kFCapW + 2u * (t0 + t)];
+    };
+    auto st = [&](int p, uint32_t t0, const u64x2& v) {
+        if (((anyf >> (2 * p)) & 3ull) == 0)
+            return;  // (wave-uniform) nothing in the pair's buckets
+        const uint32_t n0 = rdl(nw, 2 * p), n1 = 2 * p + 1 < NJ ? rdl(nw, 2 * p + 1) : 0u;
+        const uint32_t c0 = rdl(cbo, 2 * p), c1 = 2 * p + 1 < NJ ? rdl(cbo, 2 * p + 1) : 0u;
+        const uint32_t nj = half ? n1 : n0, cj = half ? c1 : c0;
+        const uint32_t q = 2u * (t0 + t);  // the lane's first word
+        const uint32_t bj0 = wave + (uint32_t)kFWaves * (uint32_t)(2 * p);
+        const __amdgpu_buffer_rsrc_t prs = uniform_rsrc(a.part1 + (uint64_t)bj0 * a.region, pair_bytes);
+        const uint32_t off = hoff + cj + q * 8u;
+        const uint64_t w0 = v.x;
+        __builtin_amdgcn_raw_buffer_store_b128(as_u32x4(v), prs, q + 2u <= nj ? off : kOOB, 0,
+                                               DQDK_FST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(w0), prs, q + 1u == nj ? off : kOOB, 0,
+                                              DQDK_FST_AUX);
+        if (!last) {  // the flushed words, for the next round's ORs
+            const uint32_t z0 = rdl(nz, 2 * p), z1 = 2 * p + 1 < NJ ? rdl(nz, 2 * p + 1) : 0u;
+            const uint32_t zj = half ? z1 : z0;
+            const uint32_t bj = wave + (uint32_t)kFWaves * ((uint32_t)(2 * p) + half);
+            if (q + 2u <= zj)
+                *(u64x2*)&lds.stage[bj * (uint32_t)kFCapW + q] = u64x2{0ull, 0ull};
+            else if (q + 1u == zj)
+                lds.stage[bj * (uint32_t)kFCapW + q] = 0ull;
+        }
+    };
+#pragma unroll 1
+    for (int h = 0; h < NP; h += GP) {
+        u64x2 v[GP];
+#pragma unroll
+        for (int g = 0; g < GP; g++)
+            if (h + g < NP)
+                rd(h + g, 0u, v[g]);
+#pragma unroll
+        for (int g = 0; g < GP; g++)
+            if (h + g < NP)
+                st(h + g, 0u, v[g]);
+    }
+    // runs past 64 words: a second pass per such pair (never in the lines
+    // policy's rounds, which flush at most two 16-word lines of a bucket)
+    if (!kLines || kLast) {
+        uint64_t m = __ballot(nw > 64u || nz > 64u);
+        while (m) {
+            const int p = (int)__builtin_ctzll(m) >> 1;
+            m &= ~(3ull << (2 * p));  // (both slots of the pair at once)
+            u64x2 v;
+            rd(p, 32u, v);
+            st(p, 32u, v);
+        }
+    }
+    // carry the remainders to the stage's start (words [w / 3, ceil(c / 3)):
+    // behind the flushed ones, so source and destination do not overlap)
+    if (!last) {
+        if (kLines) {  // up to 16 words: a wave per bucket
+            for (uint64_t m = __ballot(w != 0 && c > w); m; m &= m - 1) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                const uint32_t bj = wave + (uint32_t)kFWaves * j;
+                const uint32_t wj = rdl(w, j) / 3u, r = (rdl(c, j) + 2u) / 3u - wj;
+                uint64_t* const sg = &lds.stage[bj * (uint32_t)kFCapW];
+                uint64_t x = 0;
+                if ((uint32_t)lane < r)
+                    x = sg[wj + lane];
+                if ((uint32_t)lane < r) {
+                    sg[lane] = x;
+                    sg[wj + lane] = 0ull;
+                }
+            }
+        } else if (w != 0 && c > w) {  // one word: each lane its own bucket
+            uint64_t* const sg = &lds.stage[b * (uint32_t)kFCapW];
+            const uint64_t x = sg[w / 3u];
+            sg[0] = x;
+            sg[w / 3u] = 0ull;
+        }
+    }
+    if (b < (uint32_t)kL1Buckets) {
+        cur += fit;
         lds.scnt[b] = c - w;
+    }
 }
 
 // Two policies for the pieces' partial lines (runs end mid-line), chosen by
@@ -1362,6 +1397,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     const uint32_t wslot0 = wave * 64;
     for (int b = tid; b < kL1Buckets + 4; b += kFThreads)
         lds.scnt[b] = 0;
+    for (uint32_t q = (uint32_t)tid; q < (kStageWords + 64) / 2; q += kFThreads)  // the stage's words: zero
+        ((u64x2*)lds.stage)[q] = u64x2{0ull, 0ull};
     lds.sum[tid] = 0;
     lds.oob[tid] = 0;
     if (tid == 0)
@@ -1383,6 +1420,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     const uint32_t nsuper = (ntiles + kFWaves - 1) / kFWaves;
     const int W = (int)a.round_windows;
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
+    int kr = 0;         // windows of the current round so far: rounds run on across super-tiles
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
         const uint32_t tile = st * kFWaves + wave;
         // frame of this lane: tile-major (64 consecutive frames per wave), or
@@ -1400,8 +1438,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         phase_a<kHeadA>(a, i, live, fi, r, lf, stream, akey, na, hw);
         (void)hw;
         if (kHeadA && __ballot(na != 0)) {
-            // (the stage holds at most the last round's carry here: room for
-            // these keys, at most 7 per frame, is in the round sizing)
+            // (mid-round: rounds run on across super-tiles; keys past a
+            // full stage go to the overflow region like any others)
             fused_keys_a(a, akey, na, wslot0 + (uint32_t)lane, lds, ovf_rsrc, (uint32_t)lane);
         }
         const uint64_t smask0 = __ballot(stream);
@@ -1413,8 +1451,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
 #pragma unroll
         for (int w = 0; w < kFWaves; w++)
             tmax = max(tmax, (int)lds.wtot[w]);
-        const int rounds = (tmax + W - 1) / W;  // the same for every wave: the barriers below match
-        lds_barrier();                          // wtot is rewritten by the next super-tile
+        // the same for every wave: the barriers below match
+        const int kend = (tmax + kFRingW - 1) / kFRingW * kFRingW;
+        lds_barrier();  // wtot is rewritten by the next super-tile
 
         // ---- phase B: rounds of W windows, the block's stage flushed after each ----
         const uint32_t lane16 = (uint32_t)lane * 16u;
@@ -1456,10 +1495,10 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         else
             P = PFrame{0, 0, 0, 0, 0, 0, 0, kNoWin, kNoWin, 0, 16};
         uint32_t acc0 = 0, acc1 = 0;
-        // one loop over the rounds' windows (the flush inside it, every W
-        // windows): a single back-edge keeps the compiler's vmcnt accounting
-        // of the load ring exact across rounds
-        const int kend = rounds * W;
+        // one loop over the super-tile's windows (a flush inside it every W
+        // windows of the block's count, which runs on across super-tiles):
+        // a single back-edge keeps the compiler's vmcnt accounting of the
+        // load ring exact across rounds
         for (int k = 0; k < kend; k += kFRingW) {
 #pragma unroll
             for (int d = 0; d < kFRingW; d++) {
@@ -1488,7 +1527,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
                 fused_pair(a, b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
                 if (active && ++wp == P.nwin) {
-                    frame_sum_add(&lds.sum[wslot0 + jp], &lds.stage[kL1Buckets * kFCap + lane], acc0 + acc1,
+                    frame_sum_add(&lds.sum[wslot0 + jp], &lds.csink[lane], acc0 + acc1,
                                   (lane & 15) == 15);
                     acc0 = acc1 = 0;
                     wp = 0;
@@ -1500,7 +1539,9 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 issue(b0[d], b1[d]);
             }
-            if ((k + kFRingW) % W == 0) {  // end of a round (block-uniform)
+            kr += kFRingW;
+            if (kr == W) {  // end of a round (block-uniform)
+                kr = 0;
                 lds_barrier();
                 fused_flush<kLines, false>(a, lds, lane, wave, fcur, ovf_rsrc);
                 lds_barrier();
