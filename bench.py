@@ -127,6 +127,11 @@ def umem_size(D, n, L, stride, queue=0):
     return (int(LIB.lib().dqdk_synth_umem_size(ctypes.byref(c), n)) + 15) // 16 * 16
 
 
+def progress(msg: str) -> None:
+    """A liveness line on stderr (the JSON line alone goes to stdout)."""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="torch", image=None):
     """Synthetic UMEM for queue `queue`, generated in chunks straight into HBM
     (host memory stays one chunk); returns (d_umem, d_desc, desc, host sample,
@@ -182,8 +187,10 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     pass_records = (args.records or not histo) and not args.no_records
 
     # ---- input: queue `rank` of the synthetic UMEM replay, resident in HBM ----
+    t_in = time.time()
     d_umem, d_desc, desc, sample, owner = synth_to_device(D, torch, dev, n, L, stride, queue=rank,
                                                           alloc=args.umem_alloc, image=image)
+    progress(f"rank {rank}: {n} x {L or 'mixed'} B frames resident ({time.time() - t_in:.1f} s)")
     umem_bytes = d_umem.numel()
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
@@ -208,6 +215,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         step()
         warm_extra += 1
     probe = q.staging_probe()
+    progress(f"rank {rank}: {L or 'mixed'} B warm ({args.warmup + warm_extra} batches)")
     q.flush_histogram()  # no warmup batch left staged for the timed region's slice passes
     torch.cuda.synchronize(dev)
     q.read_timing()  # discard
