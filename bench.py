@@ -160,6 +160,8 @@ def synth_to_device(D, torch, dev, n, L, stride, queue, chunk=1 << 16, alloc="to
         descs.append(d)
         if sample is None:
             sample = (u, d.copy())  # the CPU baseline's sample: the workload's first frames
+        if (f0 // chunk) % 4 == 3:
+            progress(f"queue {queue}: {f0 + m} of {n} x {L or 'mixed'} B frames generated")
     desc = np.concatenate(descs)
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
     return d_umem, d_desc, desc, sample, owner
