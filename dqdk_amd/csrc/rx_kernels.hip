@@ -2307,34 +2307,48 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         }
     };
 
+    // The item loop keeps three barriers an item: item i's scan (its own
+    // barrier), then B2 (cursors) -> scatter -> the next item's count and the
+    // piece starts of the one after it -> B3 (stage, counts, piece starts)
+    // -> read-out of item i and the loads of item i + 2.  Invariant at the
+    // top: item's counts are complete in cnt, g is item + gridDim.x's
+    // geometry, its triples loading (gathered: nk) with its piece starts in
+    // prt[pb ^ 1].
     Item g{};
     int pb = 0;
-    if (blockIdx.x < nitems) {
-        g = geo(blockIdx.x);
+    uint32_t item = blockIdx.x;
+    if (item < nitems) {
+        g = geo(item);
         stage_pieces(g, 0);
         lds_barrier();
         if (g.gath)
             load(g, 0);
         else
             load_contig(g);
-    }
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x, pb ^= 1) {
         count(g);
-        // the next item's keys load while this one is scanned, scattered and
-        // written out
-        const bool more = item + gridDim.x < nitems;
-        if (more) {
+        if (item + gridDim.x < nitems) {
             g = geo(item + gridDim.x);
-            stage_pieces(g, pb ^ 1);
+            stage_pieces(g, 1);
         }
         lds_barrier();
-        if (more && g.gath)
-            load(g, pb ^ 1);
+        if (item + gridDim.x < nitems && g.gath)
+            load(g, 1);
+    }
+    for (; item < nitems; item += gridDim.x, pb ^= 1) {
         const uint32_t nv = scan(item);
         lds_barrier();
         scatter();
-        if (more && !g.gath)
-            load_contig(g);
+        const bool more = item + gridDim.x < nitems;
+        if (more) {
+            if (!g.gath)
+                load_contig(g);  // (a contiguous item's keys go straight to key[], which the scatter freed)
+            count(g);            // (the scan zeroed the counters)
+        }
+        const bool more2 = item + 2u * gridDim.x < nitems;
+        if (more2) {
+            g = geo(item + 2u * gridDim.x);
+            stage_pieces(g, pb);  // (prt[pb]: last read by the loads of item, long issued)
+        }
         lds_barrier();
         // item i's valid keys go to part2 [i * kPartChunk, + nv) in 16-B stores
         // (the bytes past nv in the last store are never read)
@@ -2342,8 +2356,12 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         u32x4_t* dst4 = (u32x4_t*)(a.part2 + (uint64_t)item * kPartChunk);
         for (uint32_t p = opaque((uint32_t)tid); p * 8u < nv; p += kPartThreads)
             dst4[p] = st4[p];
+        // item i + 2's triples load while item i + 1 is scanned, scattered
+        // and written out
+        if (more2 && g.gath)
+            load(g, pb);
         // (no barrier here: the stage is rewritten, and wsum and the cursors
-        // re-read, only after the next item's first barrier)
+        // re-read, only after the next item's scan barrier)
     }
     if (a.p2_ticket) {
         // every block read the counters in its prologue: the last one to
