@@ -2134,6 +2134,23 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             prk[pb][t] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + t];
         }
     };
+    // the same in two halves: the loads early (into registers), the LDS
+    // stores late, so their latency passes under the work between
+    uint32_t pst = 0, psk = 0;
+    auto fetch_pieces = [&](const Item& g) {
+        if (g.gath && (uint32_t)tid <= a.fgrid) {
+            const uint32_t t = opaque((uint32_t)tid);
+            pst = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + t];
+            psk = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + t];
+        }
+    };
+    auto put_pieces = [&](const Item& g, int pb) {
+        if (g.gath && (uint32_t)tid <= a.fgrid) {
+            const uint32_t t = opaque((uint32_t)tid);
+            prt[pb][t] = pst;
+            prk[pb][t] = psk;
+        }
+    };
     // slots: gathered items, wave w takes the item's triples [320w, 320w +
     // 320), 64 per load (load j: triple 320w + 64j + lane -> keys 3j .. 3j + 2
     // of the lane); contiguous items, keys [960w, 960w + 960), 64 per load
@@ -2337,17 +2354,24 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     for (; item < nitems; item += gridDim.x, pb ^= 1) {
         const uint32_t nv = scan(item);
         lds_barrier();
-        scatter();
+        // item i + 2's geometry and piece starts (loads now, LDS stores
+        // before the barrier: prt[pb], last read by the loads of item)
         const bool more = item + gridDim.x < nitems;
+        const bool more2 = item + 2u * gridDim.x < nitems;
+        Item g2{};
+        if (more2) {
+            g2 = geo(item + 2u * gridDim.x);
+            fetch_pieces(g2);
+        }
+        scatter();
         if (more) {
             if (!g.gath)
                 load_contig(g);  // (a contiguous item's keys go straight to key[], which the scatter freed)
             count(g);            // (the scan zeroed the counters)
         }
-        const bool more2 = item + 2u * gridDim.x < nitems;
         if (more2) {
-            g = geo(item + 2u * gridDim.x);
-            stage_pieces(g, pb);  // (prt[pb]: last read by the loads of item, long issued)
+            g = g2;
+            put_pieces(g, pb);
         }
         lds_barrier();
         // item i's valid keys go to part2 [i * kPartChunk, + nv) in 16-B stores

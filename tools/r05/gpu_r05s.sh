@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5, call s: rx_part2 with three barriers an item (the next item's
-# count and the piece starts of the one after it moved before the
-# read-out's barrier) = the in-tree build and build/ab/wt.so, against HEAD.
+# Round 5, call s/t: rx_part2 changes (s: three barriers an item; t: the piece
+# starts of item i + 2 fetched into registers before the scatter) = the
+# in-tree build and build/ab/wt.so, against HEAD.
 #   1. the -m gpu suite on the in-tree build;
 #   2. interleaved bench runs, both sizes, two rounds.
 # usage (on the GPU box): bash tools/r05/gpu_r05s.sh <tag>
