@@ -373,27 +373,30 @@ int hist_flush(dqdk_gpu_queue* q)
 // rounds (20 windows overflowed three times as many keys to rx_part1).
 //
 // The pieces' runs end mid-line.  Below 128 events per frame (1500 B) the
-// frame loads are non-temporal and the partial lines complete in L2; from
-// 128 on (9000 B: every 2-KB window full of events) whole lines are flushed
-// and remainders carried, which costs stage room, hence the smaller round
-// (A/B, one box, 9000 B: decode 2.86 -> 2.44 ms; at 1500 B lines cost 0.04 ms).
+// partial lines complete in L2 (write-back piece stores); from 128 on (9000
+// B: every 2-KB window full of events) whole lines are flushed and
+// remainders carried, which costs stage room, hence the smaller round (A/B,
+// one box, 9000 B: decode 2.86 -> 2.44 ms; at 1500 B lines cost 0.04 ms),
+// and those whole lines go out as streaming stores.  The frame loads are
+// non-temporal at both sizes (r05x/r05y, 9000 B: decode 2.06 -> 2.00 ms,
+// policy 1 -> 3, since the pieces stream).
 // policy bit 0: whole-line flushes, bit 1: non-temporal frame loads, bit 2:
 // phase A takes each frame's first line (events and checksum bytes; phase B
 // then never touches that line: traffic 2.08 -> 1.96 GB at 1M x 1500 B, but
 // the decode 0.432 -> 0.455 ms on one box, r04k2: the extra phase-A work
 // costs more than the line, so it is off by default).  The shipped library
-// holds the two default variants (1 from 128 events per frame, else 2);
+// holds the two default variants (3 from 128 events per frame, else 2);
 // a build with -DDQDK_AB_VARIANTS holds all eight, which
 // DQDK_GPU_FUSED_POLICY=<0..7> selects at queue creation (A/B, tests).
 #ifndef DQDK_FUSED_POLICY
-#define DQDK_FUSED_POLICY (E >= 128 ? 1u : 2u)
+#define DQDK_FUSED_POLICY (E >= 128 ? 3u : 2u)
 #endif
 uint32_t fused_policy_default(uint32_t E) { return (uint32_t)(DQDK_FUSED_POLICY); }
 
 #ifdef DQDK_AB_VARIANTS
 constexpr uint32_t kFusedPolicies = 0xffu;  // every variant built
 #else
-constexpr uint32_t kFusedPolicies = (1u << 1) | (1u << 2);
+constexpr uint32_t kFusedPolicies = (1u << 2) | (1u << 3);
 #endif
 
 uint32_t fused_round_windows(uint32_t E, double fill)
@@ -622,11 +625,11 @@ int probe_step(dqdk_gpu_queue* q, uint32_t n)
 void (*fused_kernel(uint32_t pol))(RxArgs)
 {
     switch (pol) {
-    case 1: return rx_decode_fused_kernel<0, true, false>;
     case 2: return rx_decode_fused_kernel<2, false, false>;
+    case 3: return rx_decode_fused_kernel<2, true, false>;
 #ifdef DQDK_AB_VARIANTS
     case 0: return rx_decode_fused_kernel<0, false, false>;
-    case 3: return rx_decode_fused_kernel<2, true, false>;
+    case 1: return rx_decode_fused_kernel<0, true, false>;
     case 4: return rx_decode_fused_kernel<0, false, true>;
     case 5: return rx_decode_fused_kernel<0, true, true>;
     case 6: return rx_decode_fused_kernel<2, false, true>;

@@ -1589,13 +1589,13 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         fold_publish(a, lds, tid);
 }
 
-// the shipped variants (fused_policy_default: 1 from 128 events per frame,
+// the shipped variants (fused_policy_default: 3 from 128 events per frame,
 // else 2); the A/B build (-DDQDK_AB_VARIANTS) holds the other six as well
-template __global__ void rx_decode_fused_kernel<0, true, false>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, false, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<2, true, false>(RxArgs);
 #ifdef DQDK_AB_VARIANTS
 template __global__ void rx_decode_fused_kernel<0, false, false>(RxArgs);
-template __global__ void rx_decode_fused_kernel<2, true, false>(RxArgs);
+template __global__ void rx_decode_fused_kernel<0, true, false>(RxArgs);
 template __global__ void rx_decode_fused_kernel<0, false, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<0, true, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, false, true>(RxArgs);

@@ -1,8 +1,9 @@
 """The fused decode's variants vs the oracle on frames built to hit every
-edge of its geometry.  The shipped library holds policies 1 and 2 (whole-line
-flushes / non-temporal loads, the defaults from and below 128 events per
-frame); the first-line hand-off (policy bit 2) and the other A/B variants are
-in a -DDQDK_AB_VARIANTS build only, and their cases skip on the shipped one.
+edge of its geometry.  The shipped library holds policies 3 and 2 (whole-line
+flushes / whole-word flushes, both with non-temporal frame loads: the
+defaults from and below 128 events per frame); the first-line hand-off
+(policy bit 2) and the other A/B variants are in a -DDQDK_AB_VARIANTS build
+only, and their cases skip on the shipped one.
 
 Phase A reads each frame's first 128 B for the headers; with the hand-off it
 also decodes the events and sums the checksum bytes of that line, and the
@@ -112,7 +113,7 @@ def _policy_or_skip(policy, monkeypatch):
         raise
 
 
-@pytest.mark.parametrize("policy", ["1", "2", "6", "4", "5", "7"])
+@pytest.mark.parametrize("policy", ["3", "2", "6", "1", "4", "5", "7"])
 @pytest.mark.parametrize("payloadsz", [1458, 48, 16])
 @pytest.mark.parametrize("flags", [D.F_CSUM, 0], ids=["csum", "nocsum"])
 def test_fused_first_line_handoff_vs_oracle(policy, payloadsz, flags, monkeypatch):
@@ -168,7 +169,7 @@ def test_folded_counters_vs_oracle(fold, flags, monkeypatch):
         assert ocnt["invalid_udp_pkts"] > 0
 
 
-@pytest.mark.parametrize("policy", ["2", "1", "6"])
+@pytest.mark.parametrize("policy", ["2", "3", "1", "6"])
 @pytest.mark.parametrize("fmap", ["1", "0"])
 def test_frame_maps_vs_oracle(policy, fmap, monkeypatch):
     """Both frame maps of the fused decode (tile-major: a wave streams 64
