@@ -212,7 +212,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     # fused batches try candidate piece buffers, the next keeps the fastest)
     # belongs to the warmup: extra untimed batches until it has decided
     warm_extra = 0
-    while q.staging_probe()["chosen"] < 0 and warm_extra < 8 and n >= 65536 and histo and E and \
+    while q.staging_probe()["chosen"] < 0 and warm_extra < 16 and n >= 65536 and histo and E and \
             not pass_records:
         step()
         warm_extra += 1

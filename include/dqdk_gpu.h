@@ -400,7 +400,7 @@ const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
  * *chosen = the kept candidate (-1: not decided yet or off), ns_per_frame[k]
  * = candidate k's best decode time per frame (0: untimed), k < ncand.
  * Returns the number of candidates. */
-#define DQDK_GPU_PROBE_CANDS 3
+#define DQDK_GPU_PROBE_CANDS 5
 int dqdk_gpu_queue_staging_probe(dqdk_gpu_queue_t* q, int* chosen, float* ns_per_frame, int ncand);
 
 const char* dqdk_gpu_last_error(void);
