@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5, call ac: the slice pass gathers with two register sets in turn
+# (group g + 1's loads in flight while group g is counted; the low-byte plane
+# loaded after the gather instead of held across it) = the in-tree build and
+# build/ab/wt.so; wt2 = the same with two items per wave group (kNI 2);
+# against HEAD (head).
+#   1. the -m gpu suite on the in-tree build;
+#   2. interleaved bench runs, both sizes, three rounds.
+# usage (on the GPU box): bash tools/r05/gpu_r05ac.sh <tag>
+set -e
+tag=${1:-r05ac}
+mkdir -p gpurun_out/ab_${tag}_1500 gpurun_out/ab_${tag}_9000
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+    > gpurun_out/pytest_$tag.log 2>&1
+for r in 1 2 3; do
+    for L in 1500 9000; do
+        for v in head wt wt2; do
+            DQDK_GPU_LIB=$PWD/build/ab/$v.so timeout -k 10 200 python3 bench.py --frame-len $L --steps 10 \
+                --warmup 2 --no-cpu-baseline --no-9000 --no-box-state > gpurun_out/ab_${tag}_$L/${v}_$r.json \
+                2> gpurun_out/ab_${tag}_$L/${v}_$r.err
+        done
+    done
+done
