@@ -1388,9 +1388,19 @@ int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size)
     if (!q || !umem || !size)
         return -EINVAL;
     SETDEV(q->device);
-    for (auto& r : q->regs)
-        if (r.host == umem)
+    for (size_t k = 0; k < q->regs.size(); k++) {
+        if (q->regs[k].host != umem)
+            continue;
+        if (q->regs[k].size >= size)
             return 0;
+        // the same address with more bytes (a larger buffer in the old one's
+        // place, or a grown view): the old registration is replaced, never
+        // reused past its end
+        HIPCHK(hipStreamSynchronize(q->stream));
+        HIPCHK(hipHostUnregister(umem));
+        q->regs.erase(q->regs.begin() + (long)k);
+        break;
+    }
     HIPCHK(hipHostRegister(umem, size, hipHostRegisterMapped));
     void* dev = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dev, umem, 0);
@@ -1441,7 +1451,11 @@ int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_si
         int rc = dqdk_gpu_umem_register(q, (void*)umem, umem_size);
         if (rc)
             return rc;
-        reg = &q->regs.back();
+        for (auto& r : q->regs)
+            if ((const uint8_t*)r.host <= umem && umem + umem_size <= (const uint8_t*)r.host + r.size)
+                reg = &r;
+        if (!reg)
+            return fail_errno(-EINVAL, "rx_batch: umem not covered by its registration");
     }
     const uint8_t* dev_umem = (const uint8_t*)reg->dev + (umem - (const uint8_t*)reg->host);
     if (q->raw_fd < 0) {

@@ -190,7 +190,11 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
 /* umem: host UMEM (pinned once through dqdk_gpu_umem_register for best
  * rate); d, per_pkt, delta: host pointers.  Copies the batch's frames in,
  * runs the batch, copies per-frame results and this batch's counter delta
- * out.  Returns 0, or the negative errno of the first failure. */
+ * out.  Returns 0, or the negative errno of the first failure.
+ * dqdk_gpu_umem_register is a no-op for an address already registered with
+ * at least `size` bytes; with fewer, the old registration is replaced (the
+ * queue's stream drained first).  rx_batch registers a UMEM no registration
+ * covers. */
 int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size);
 int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
 int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,

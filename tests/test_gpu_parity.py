@@ -266,6 +266,31 @@ def test_host_dropin_api_matches_device_api():
     assert total["rcvd_pkts"] == 2 * ocnt["rcvd_pkts"]
 
 
+def test_host_dropin_grown_umem_at_the_same_address():
+    """A UMEM registered by a first batch, then a larger one at the same
+    address (a grown view of one buffer): the second batch's frames past the
+    first registration are read through a registration that covers them (the
+    old one is replaced, not reused past its end), and both batches equal the
+    oracle."""
+    _need_gpu()
+    umem, desc = D.synth_umem(2048, 1500, 4096, faulty=True)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
+    half = len(desc) // 2
+    small, d_small = umem[: half * 4096], desc[:half]
+    ores1, ocnt1, _ = O.rx_batch(small.copy(), d_small, cfg.payloadsz, cfg.mode, cfg.flags)
+    ores2, ocnt2, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags)
+    with D.RxQueue(0, cfg, 4096) as q:
+        res1, delta1 = q.process_batch(small, d_small)
+        res2, delta2 = q.process_batch(umem, desc)
+        q.unregister_umem(umem)
+    np.testing.assert_array_equal(res1, ores1)
+    np.testing.assert_array_equal(res2, ores2)
+    for k, v in ocnt1.items():
+        assert delta1[k] == v, k
+    for k, v in ocnt2.items():
+        assert delta2[k] == v, k
+
+
 def test_histogram_accumulates_across_batches_and_merges():
     _need_gpu()
     cfg = D.RxConfig(payloadsz=1458)
