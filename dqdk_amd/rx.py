@@ -69,12 +69,17 @@ class RxQueue:
         L.check(L.lib().dqdk_gpu_queue_create(device, C.byref(cfg.to_c()), max_batch, C.byref(h)),
                 "dqdk_gpu_queue_create")
         self._h = h
+        # host UMEMs the queue holds registered, by address: kept alive until
+        # unregistered (a freed registered buffer would leave its registration
+        # to a new buffer at the same address)
+        self._pinned = {}
 
     # -- lifecycle ---------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_h", None):
             L.lib().dqdk_gpu_queue_destroy(self._h)
             self._h = None
+            self._pinned = {}
 
     def __enter__(self):
         return self
@@ -123,6 +128,7 @@ class RxQueue:
         n = len(desc)
         res = np.zeros(n, dtype=L.RESULT_DTYPE)
         delta = L.Counters()
+        self._keep(umem)  # (registered on first use)
         L.check(L.lib().dqdk_gpu_rx_batch(self._h, umem.ctypes.data, umem.nbytes, desc.ctypes.data, n,
                                           res.ctypes.data, C.byref(delta)), "dqdk_gpu_rx_batch")
         return res, delta.as_dict()
@@ -159,9 +165,17 @@ class RxQueue:
 
     def register_umem(self, umem: np.ndarray) -> None:
         L.check(L.lib().dqdk_gpu_umem_register(self._h, umem.ctypes.data, umem.nbytes), "umem_register")
+        self._keep(umem)
+
+    def _keep(self, umem: np.ndarray) -> None:
+        """Hold the largest buffer seen at the address (a view keeps its base)."""
+        cur = self._pinned.get(umem.ctypes.data)
+        if cur is None or cur.nbytes < umem.nbytes:
+            self._pinned[umem.ctypes.data] = umem
 
     def unregister_umem(self, umem: np.ndarray) -> None:
         L.check(L.lib().dqdk_gpu_umem_unregister(self._h, umem.ctypes.data), "umem_unregister")
+        self._pinned.pop(umem.ctypes.data, None)
 
     # -- egress ------------------------------------------------------------
     def counters(self) -> dict:
