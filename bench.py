@@ -70,6 +70,9 @@ def parse_args(argv=None):
     p.add_argument("--records", action="store_true",
                    help="histogram mode: also write frame-order decoded records (the unfused path)")
     p.add_argument("--no-9000", action="store_true", help="default run: skip the by_frame_len 9000 B measurement")
+    p.add_argument("--no-configs", action="store_true",
+                   help="default run: skip the by_config lines (BASELINE configs[1], [2], [3]'s mixed batch)")
+    p.add_argument("--rotate", type=int, default=1, help="R copies of the UMEM image, batch k reads copy k %% R")
     p.add_argument("--e2e", action="store_true", help="PCIe-inclusive pipeline (configs[4])")
     p.add_argument("--e2e-frames", type=int, default=1 << 16, help="frames per e2e batch")
     p.add_argument("--offered-gbps", type=float, default=100.0, help="e2e offered load over all queues (Gbit/s)")
@@ -194,6 +197,14 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                                                           alloc=args.umem_alloc, image=image)
     progress(f"rank {rank}: {n} x {L or 'mixed'} B frames resident ({time.time() - t_in:.1f} s)")
     umem_bytes = d_umem.numel()
+    # --rotate R: R copies of the image, batch k reads copy k % R, so a
+    # working set the 256 MB MALL could hold is not re-read from it
+    # (256K x 1500 B touches 384 MB of frame bytes)
+    rot = [D.DeviceBuffer(dev.index, umem_bytes) for _ in range(max(getattr(args, "rotate", 1), 1) - 1)]
+    umems = [d_umem.data_ptr()]
+    for b in rot:
+        b.tensor[:umem_bytes].copy_(d_umem)
+        umems.append(b.ptr)
     d_res = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     d_keys = torch.zeros(max(n * E, 1), dtype=torch.int32, device=dev)
     frame_bytes = int(desc["len"].astype(np.int64).sum())  # per batch (n * L unless mixed)
@@ -202,8 +213,12 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     stream = torch.cuda.current_stream(dev)
     q.set_stream(stream.cuda_stream)
 
+    nstep = [0]
+
     def step():
-        q.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
+        ptr = umems[nstep[0] % len(umems)]
+        nstep[0] += 1
+        q.process_device(ptr, umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
                          d_keys.data_ptr() if pass_records else None)
 
     for _ in range(args.warmup):
@@ -245,8 +260,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     t1 = time.perf_counter()
     q.enable_timing(False)
     stages = q.read_timing()
-    elapsed, per_rank = aggregate_ranks(torch, dist, dev, world, t1 - t0, t_rank, n * args.steps,
-                                        frame_bytes * args.steps)
+    elapsed = aggregate_ranks(torch, dist, dev, world, t1 - t0)
 
     # correctness guard on the measured batch (cheap, outside the timed region)
     cnt = q.counters()
@@ -380,7 +394,17 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                 "umem_image": {"alloc": args.umem_alloc,
                                "contiguous": bool(owner.contiguous) if owner is not None else False,
                                "va": hex(d_umem.data_ptr()),
-                               "va_mod_2MiB": d_umem.data_ptr() % (2 << 20), "bytes": umem_bytes}}
+                               "va_mod_2MiB": d_umem.data_ptr() % (2 << 20), "bytes": umem_bytes,
+                               "rotated_copies": len(umems)}}
+
+    # ---- this rank's report, gathered on rank 0 (N > 1) ----
+    report = {"rank": rank, "Mpkt_s": round(n * args.steps / t_rank / 1e6, 3),
+              "frame_GB_s": round(frame_bytes * args.steps / t_rank / 1e9, 2),
+              "decode_ms": dec.get("avg_ms"), "decode_alg_bytes": alg["rx_decode"],
+              "decode_frac": dec.get("frac_hbm"), "decode_kernel": roofline["kernel"],
+              "frac_of_measured_stream": roofline["frac_of_measured_stream"],
+              "staging_probe": dict(probe, warmup_extra=warm_extra), "bdf": device_bdf(torch, dev.index)}
+    per_rank = gather_rank_reports(dist, world, report)
 
     # ---- CPU baseline: the oracle (C restatement), rank 0, outside the timed region ----
     cpu = None
@@ -391,8 +415,10 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
 
     q.close()
     del d_umem, d_desc, d_res, d_keys
+    torch.cuda.synchronize(dev)
+    for b in rot:
+        b.close()
     if owner is not None and image is None:
-        torch.cuda.synchronize(dev)
         owner.close()
     torch.cuda.empty_cache()
     return {
@@ -408,6 +434,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                    "parallelism": f"queue-per-gpu x{world}" + (" (shared-GPU rehearsal)" if args.share_gpu else "")},
         "frame_GB_s": round(frame_gbs, 2),
         "per_gpu": per_rank,
+        "roofline_all_gpus": aggregate_roofline(per_rank),
         "step_ms_median": round(step_ms[len(step_ms) // 2], 4),
         "step_ms_min": round(step_ms[0], 4),
         "kernels": st,
@@ -418,6 +445,35 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         # candidate's decode ns per frame, untimed warmup batches it added
         "staging_probe": dict(probe, warmup_extra=warm_extra),
     }
+
+
+# BASELINE.json configs measured beside the headline, each
+# through the same measure() as the headline: its own kernels, roofline
+# (SURVEY §8(d) bytes: 16 + L + 8 per frame, + 4 B per event when events are
+# decoded) and CPU baseline.  (name, BASELINE config, overrides, frame_len)
+BY_CONFIG = [
+    # parse + IPv4/UDP checksum only, no event work (no histogram, no records):
+    # 1,524 B per frame; 4 rotated image copies (1.5 GB of frame bytes a
+    # cycle) so the 384 MB the batch touches is not served from the MALL
+    ("parse_csum_256Kx1500", "configs[1]", {"frames": 1 << 18, "no_histo": True, "no_records": True, "rotate": 4},
+     1500),
+    ("jumbo_256Kx9000", "configs[2]", {"frames": 1 << 18}, 9000),
+    ("mixed_1Mx1500_9000", "configs[3] (one queue of its mixed traffic)", {"frames": 1 << 20}, 0),
+]
+
+
+def by_config(args, torch, dist, dev, rank, world, local, cpu_sec):
+    out = {}
+    for name, which, over, L in BY_CONFIG:
+        a2 = argparse.Namespace(**vars(args))
+        for k, v in over.items():
+            setattr(a2, k, v)
+        a2.stride = 0
+        a2.payloadsz = 0
+        r = measure(a2, L, torch, dist, dev, rank, world, local, min(cpu_sec, 2.0))
+        r["baseline_config"] = which
+        out[name] = r
+    return out
 
 
 def box_state(torch, dev_index):
@@ -470,20 +526,52 @@ def box_state(torch, dev_index):
     return out
 
 
-def aggregate_ranks(torch, dist, dev, world, elapsed, t_rank, packets, frame_bytes):
-    """Job time = max over ranks of the barrier-bracketed time; per-GPU rates
-    from each rank's own time.  Returns (elapsed, per_gpu list or None)."""
+def aggregate_ranks(torch, dist, dev, world, elapsed):
+    """Job time = max over ranks of the barrier-bracketed time."""
     if world == 1:
-        return elapsed, None
+        return elapsed
     if dist.get_backend() == "gloo":
         dev = torch.device("cpu")
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    mine = torch.tensor([packets / t_rank / 1e6, frame_bytes / t_rank / 1e9], dtype=torch.float64, device=dev)
-    allr = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(allr, mine)
-    return float(t.item()), [{"rank": r, "Mpkt_s": round(float(v[0]), 3), "frame_GB_s": round(float(v[1]), 2)}
-                             for r, v in enumerate(allr)]
+    return float(t.item())
+
+
+def gather_rank_reports(dist, world, report):
+    """Every rank's own report (rank 0 gets the list; None at N = 1): its
+    packets and frame bytes over its own time, its roofline kernel's time,
+    algorithmic bytes and fraction, its staging-probe choice and candidate
+    times, its GPU's PCI id -- so a slow rank in an N-GPU line is visible
+    (the reference runs one worker per queue,
+    src/dqdk.c:517-620)."""
+    if world == 1:
+        return None
+    out = [None] * world
+    dist.all_gather_object(out, report)
+    return out
+
+
+def aggregate_roofline(reports, peak=HBM_PEAK_GBS):
+    """The N-GPU roofline: every rank's roofline-kernel algorithmic bytes per
+    launch, summed, over the slowest rank's launch time, against N x peak."""
+    if not reports or any(r.get("decode_ms") in (None, 0) for r in reports):
+        return None
+    n = len(reports)
+    alg = sum(r["decode_alg_bytes"] for r in reports)
+    t = max(r["decode_ms"] for r in reports) * 1e-3
+    gbs = alg / t / 1e9
+    fr = [r["decode_frac"] for r in reports]
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": peak * n, "unit": "GB/s",
+            "frac": round(gbs / (peak * n), 4), "per_rank_frac": fr, "min_rank_frac": min(fr),
+            "slowest_rank": max(range(n), key=lambda k: reports[k]["decode_ms"])}
+
+
+def device_bdf(torch, dev_index):
+    try:
+        pr = torch.cuda.get_device_properties(dev_index)
+        return "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+    except Exception as e:  # noqa: BLE001
+        return f"<{type(e).__name__}>"
 
 
 def dry_run(args, torch, dist, dev, rank, world):
@@ -498,10 +586,19 @@ def dry_run(args, torch, dist, dev, rank, world):
     t_rank = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed, per_rank = aggregate_ranks(torch, dist, dev, world, time.perf_counter() - t0, t_rank,
-                                        args.frames * args.steps, args.frames * 1500 * args.steps)
+    elapsed = aggregate_ranks(torch, dist, dev, world, time.perf_counter() - t0)
+    # the same report a GPU rank gives, from the sleep: "decode" = one step
+    dec_ms = t_rank / args.steps * 1e3
+    alg = args.frames * (16 + 1500 + 8 + 4 * 91)
+    rep = {"rank": rank, "Mpkt_s": round(args.frames * args.steps / t_rank / 1e6, 3),
+           "frame_GB_s": round(args.frames * 1500 * args.steps / t_rank / 1e9, 2),
+           "decode_ms": round(dec_ms, 4), "decode_alg_bytes": alg,
+           "decode_frac": round(alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+           "staging_probe": {"chosen": -1, "ns_per_frame": []}, "bdf": "dry-run"}
+    reports = gather_rank_reports(dist, world, rep)
     return {"value": round(args.frames * args.steps * world / elapsed / 1e6, 3),
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "per_gpu": per_rank,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "per_gpu": reports,
+            "roofline_all_gpus": aggregate_roofline(reports),
             "config": {"workload": "dry run (no GPU work)", "parallelism": f"queue-per-gpu x{world}"}}
 
 
@@ -536,10 +633,21 @@ def cpu_baseline(sample, cfg, histo, budget_sec, world):
         pass
     # one worker thread per queue: the N-queue comparison is N threads
     t_match = str(min(world, 8)) if str(min(world, 8)) in threads else "1"
+    l3 = ""
+    try:
+        l3 = Path("/sys/devices/system/cpu/cpu0/cache/index3/size").read_text().strip()
+    except OSError:
+        pass
+    fbytes = int(desc["len"].astype(np.int64).sum())
     return {"value": threads[t_match], "unit": "Mpkt/s", "cores": int(t_match), "kind": "port",
-            "sample": f"first {len(desc)} frames of the workload; 1 thread x {passes} passes ({sec:.1f} s); "
-                      f"2/4/8 threads split the same frames; histogram {'on (2.38 GB table)' if histo else 'off'}; "
+            "sample": f"first {len(desc)} frames of the workload ({fbytes / 1e6:.0f} MB of frame bytes in a "
+                      f"{umem.nbytes / 1e6:.0f} MB UMEM copy), re-read every pass: 1 thread x {passes} passes "
+                      f"({sec:.1f} s); 2/4/8 threads split the same frames, so the 8-thread figure reads a "
+                      f"sample that can stay resident in the host's caches (L3 {l3 or '?'} per CCD, several "
+                      f"CCDs) across passes -- an upper bound for the CPU, not an HBM-sized stream; histogram "
+                      f"{'on (2.38 GB table, random updates: not cache-resident)' if histo else 'off'}; "
                       f"host {model}, nproc {os.cpu_count()}",
+            "sample_frames": len(desc), "sample_frame_bytes": fbytes, "host_l3": l3,
             "threads_Mpkt_s": threads}
 
 
@@ -651,6 +759,8 @@ def main():
             extra = {"by_frame_len": {"1500": {"value": r["value"], "frame_GB_s": r["frame_GB_s"],
                                                "ms_per_step": r["ms_per_step"]},
                                       "9000": r9}}
+            if not args.no_configs:
+                extra["by_config"] = by_config(args, torch, dist, dev, rank, world, local, cpu_sec)
 
     for im in images.values():
         torch.cuda.synchronize(dev)

@@ -1,6 +1,7 @@
 """Build the in-tree native libraries (gfx950 HIP + host C).
 
-Outputs (git-ignored; all travel to the GPU box with the gpurun snapshot):
+Outputs (git-ignored; the first three travel to the GPU box with the gpurun
+snapshot, oracle/_ref/ stays in this container: .gpurunignore lists it):
   dqdk_amd/lib/libdqdk_gpu.so   -- the product: HIP kernels + C ABI (include/dqdk_gpu.h)
   oracle/liboracle.so           -- test-only C restatement (oracle/Makefile)
   build/fetch_xsk_harness       -- test-only C consumer of include/dqdk_gpu.h (tests/c/)

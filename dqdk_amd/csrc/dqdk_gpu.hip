@@ -596,11 +596,22 @@ int probe_step(dqdk_gpu_queue* q, uint32_t n)
     }
     if (q->probe == 1) {  // the candidates, allocated beside the original (other physical pages)
         q->part1_cand[0] = q->d_part1;
-        for (int k = 1; k < kProbeCands; k++)
-            if (dev_alloc(&q->part1_cand[k], q->part1_elems * 4, q->alloc_kind) != hipSuccess) {
+        // one at a time, and only while at least as much device memory as
+        // the candidate stays free (several GB each at 1M x 9000 B,
+        // times the queues sharing a GPU); a candidate that does not fit is
+        // simply not probed
+        const uint64_t bytes = q->part1_elems * 4;
+        for (int k = 1; k < kProbeCands; k++) {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < 2 * bytes) {
+                (void)hipGetLastError();
+                break;
+            }
+            if (dev_alloc(&q->part1_cand[k], bytes, q->alloc_kind) != hipSuccess) {
                 (void)hipGetLastError();
                 q->part1_cand[k] = nullptr;
             }
+        }
         if ((!q->probe_ev[0] && hipEventCreate(&q->probe_ev[0]) != hipSuccess) ||
             (!q->probe_ev[1] && hipEventCreate(&q->probe_ev[1]) != hipSuccess)) {
             (void)hipGetLastError();
@@ -1104,7 +1115,9 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         q->histo_path = 2;
 
     auto cleanup = [&](int rc) {
-        dqdk_gpu_queue_destroy(q);
+        const std::string why = g_err;  // (the creation failure is the one reported)
+        (void)dqdk_gpu_queue_destroy(q);
+        g_err = why;
         return rc;
     };
     hipError_t e;
@@ -1252,7 +1265,7 @@ int dqdk_gpu_device_free(int device, void* d_ptr)
                 break;
             }
     }
-    dev_free(d_ptr);
+    HIPCHK(hipFree(d_ptr));
     return 0;
 }
 
@@ -1261,71 +1274,100 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     if (!q)
         return -EINVAL;
     DevGuard dev_guard_(q->device);
+    // Every call is checked and the first failure returned, naming the call
+    // (a fault in a queue's last work or in its teardown must
+    // fail the caller that destroys it, not surface at some later copy).
+    // Everything is still released whatever fails.
     int rc = 0;
-    if (q->raw_fd >= 0 && (rc = raw_drain(q)) != 0)  // the last batch's raw stream still goes to its file
-        fprintf(stderr, "dqdk_gpu_queue_destroy: the last deferred raw batch was not written to fd %d: %s\n",
-                q->raw_fd, strerror(-rc));
+    std::string first;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && !rc) {
+            first = std::string("queue_destroy: ") + what + ": " + hipGetErrorString(e);
+            rc = -EIO;
+        }
+    };
+    if (dev_guard_.e != hipSuccess)
+        chk(dev_guard_.e, "hipSetDevice");
+    if (q->raw_fd >= 0) {  // the last batch's raw stream still goes to its file
+        const int wrc = raw_drain(q);
+        if (wrc) {
+            fprintf(stderr, "dqdk_gpu_queue_destroy: the last deferred raw batch was not written to fd %d: %s\n",
+                    q->raw_fd, strerror(-wrc));
+            if (!rc) {
+                first = "queue_destroy: raw drain: " + g_err;
+                rc = wrc;
+            }
+        }
+    }
     if (q->stream)
-        (void)hipStreamSynchronize(q->stream);
+        chk(hipStreamSynchronize(q->stream), "hipStreamSynchronize(queue stream)");
     if (q->raw_stream)
-        (void)hipStreamSynchronize(q->raw_stream);  // no D2H into h_rawb may outlive it
+        chk(hipStreamSynchronize(q->raw_stream), "hipStreamSynchronize(raw stream)");  // no D2H into h_rawb may outlive it
     for (auto& r : q->regs)
-        (void)hipHostUnregister(r.host);
+        chk(hipHostUnregister(r.host), "hipHostUnregister(umem)");
     for (auto& p : q->pending) {
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
+        chk(hipEventDestroy(p.a), "hipEventDestroy(timing)");
+        chk(hipEventDestroy(p.b), "hipEventDestroy(timing)");
     }
     for (auto ev : q->ev_free)
-        (void)hipEventDestroy(ev);
-    dev_free(q->d_hist);
-    dev_free(q->d_lo);
-    dev_free(q->d_snap);
-    (void)hipFree(q->d_cum);
-    (void)hipFree(q->d_batch);
-    (void)hipFree(q->d_blkcnt);
-    dev_free(q->d_keys);
+        chk(hipEventDestroy(ev), "hipEventDestroy(timing)");
+    auto dfree = [&](void* p, const char* what) {
+        if (p)
+            chk(hipFree(p), what);
+    };
+    auto hfree = [&](void* p, const char* what) {
+        if (p)
+            chk(hipHostFree(p), what);
+    };
+    dfree(q->d_hist, "hipFree(table)");
+    dfree(q->d_lo, "hipFree(table low plane)");
+    dfree(q->d_snap, "hipFree(table snapshot)");
+    dfree(q->d_cum, "hipFree(counters)");
+    dfree(q->d_batch, "hipFree(batch scratch)");
+    dfree(q->d_blkcnt, "hipFree(fold accumulators)");
+    dfree(q->d_keys, "hipFree(records)");
     for (int k = 0; k < kProbeCands; k++)
         if (q->part1_cand[k] && q->part1_cand[k] != q->d_part1)
-            dev_free(q->part1_cand[k]);
-    dev_free(q->d_part1);
+            dfree(q->part1_cand[k], "hipFree(probe candidate)");
+    dfree(q->d_part1, "hipFree(pieces)");
     for (auto ev : q->probe_ev)
         if (ev)
-            (void)hipEventDestroy(ev);
-    dev_free(q->d_part1_rec);
-    (void)hipFree(q->d_ovf);
-    dev_free(q->d_part2);
-    dev_free(q->d_runs);
-    dev_free(q->d_hscratch);
-    (void)hipFree(q->d_fix);
-    (void)hipFree(q->d_desc);
-    (void)hipFree(q->d_res);
-    (void)hipFree(q->d_raw_blk);
+            chk(hipEventDestroy(ev), "hipEventDestroy(probe)");
+    dfree(q->d_part1_rec, "hipFree(records part1)");
+    dfree(q->d_ovf, "hipFree(overflow list)");
+    dfree(q->d_part2, "hipFree(part2 staging)");
+    dfree(q->d_runs, "hipFree(part2 runs)");
+    dfree(q->d_hscratch, "hipFree(slot scratch)");
+    dfree(q->d_fix, "hipFree(fixup list)");
+    dfree(q->d_desc, "hipFree(descriptors)");
+    dfree(q->d_res, "hipFree(results)");
+    dfree(q->d_raw_blk, "hipFree(raw offsets)");
     for (int k = 0; k < 2; k++) {
-        (void)hipFree(q->d_rawb[k]);
-        if (q->h_rawb[k])
-            (void)hipHostFree(q->h_rawb[k]);
+        dfree(q->d_rawb[k], "hipFree(raw buffer)");
+        hfree(q->h_rawb[k], "hipHostFree(raw buffer)");
         if (q->raw_ev_d2h[k])
-            (void)hipEventDestroy(q->raw_ev_d2h[k]);
+            chk(hipEventDestroy(q->raw_ev_d2h[k]), "hipEventDestroy(raw)");
     }
-    if (q->h_raw_total)
-        (void)hipHostFree(q->h_raw_total);
-    if (q->h_desc)
-        (void)hipHostFree(q->h_desc);
-    if (q->h_res)
-        (void)hipHostFree(q->h_res);
-    if (q->h_batch)
-        (void)hipHostFree(q->h_batch);
+    hfree(q->h_raw_total, "hipHostFree(raw total)");
+    hfree(q->h_desc, "hipHostFree(pinned descriptors)");
+    hfree(q->h_res, "hipHostFree(pinned results)");
+    hfree(q->h_batch, "hipHostFree(pinned counters)");
     if (q->ev_read)
-        (void)hipEventDestroy(q->ev_read);
+        chk(hipEventDestroy(q->ev_read), "hipEventDestroy(ev_read)");
     if (q->raw_stream)
-        (void)hipStreamDestroy(q->raw_stream);
+        chk(hipStreamDestroy(q->raw_stream), "hipStreamDestroy(raw stream)");
     if (q->switch_ev)
-        (void)hipEventDestroy(q->switch_ev);
-    (void)hipFree(q->d_async);
+        chk(hipEventDestroy(q->switch_ev), "hipEventDestroy(switch)");
+    dfree(q->d_async, "hipFree(async bursts)");
     if (q->own_stream)
-        (void)hipStreamDestroy(q->own_stream);
+        chk(hipStreamDestroy(q->own_stream), "hipStreamDestroy(queue stream)");
+    // and nothing of the device's still-running work faulted: a sticky error
+    // of this queue's kernels or copies is reported here, by the destroy
+    chk(hipDeviceSynchronize(), "hipDeviceSynchronize");
     delete q;
-    return 0;
+    if (rc)
+        g_err = first;
+    return rc;
 }
 
 int dqdk_gpu_queue_set_stream(dqdk_gpu_queue_t* q, void* s)

@@ -96,11 +96,14 @@ struct DevScope {  // make `dev` current, restore the caller's on exit
     }
 };
 
-void fp_close(FpWorker* s)
+// Returns the queue's sync / destroy result (a fault of the worker's last
+// work fails fp_fini, not a later call).
+int fp_close(FpWorker* s)
 {
+    int rc = 0;
     if (s->q) {
         DevScope g(s->device);
-        (void)dqdk_gpu_queue_sync(s->q);
+        rc = dqdk_gpu_queue_sync(s->q);
         for (uint32_t k = 0; k < kFpMaxSlots; k++)
             if (s->ev[k])
                 (void)hipEventDestroy(s->ev[k]);
@@ -110,9 +113,12 @@ void fp_close(FpWorker* s)
             (void)hipHostFree(s->h_stage);
         if (s->h_len)
             (void)hipHostFree(s->h_len);
-        (void)dqdk_gpu_queue_destroy(s->q);
+        const int drc = dqdk_gpu_queue_destroy(s->q);
+        if (!rc)
+            rc = drc;
     }
     *s = FpWorker{};
+    return rc;
 }
 
 // Queue, pinned slots and device buffers of a new worker (under g_mu).
@@ -166,7 +172,7 @@ FpWorker* find_or_open(const void* key, int device, int* rc)
     w->key = key;
     w->device = device >= 0 ? device : next_device();
     if ((*rc = fp_open(w.get())) != 0) {
-        fp_close(w.get());
+        (void)fp_close(w.get());
         return nullptr;
     }
     g_workers.push_back(std::move(w));
@@ -405,8 +411,11 @@ int dqdk_gpu_fp_fini(uint32_t* host_hist, int csv_fd, dqdk_gpu_counters_t* total
                 rc = dqdk_gpu_histogram_write_csv(w0->q, csv_fd, nullptr);
         }
     }
-    for (auto& w : g_workers)
-        fp_close(w.get());
+    for (auto& w : g_workers) {
+        const int crc = fp_close(w.get());
+        if (!rc)
+            rc = crc;
+    }
     g_workers.clear();
     g_init = false;
     g_gen.fetch_add(1, std::memory_order_acq_rel);

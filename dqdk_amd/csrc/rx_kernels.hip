@@ -1188,6 +1188,39 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
     }
 }
 
+#ifndef DQDK_CEIL
+#define DQDK_CEIL 0
+#endif
+#if DQDK_CEIL
+// Timing-only CEILING of the fused decode's read + write pattern (VERDICT r5
+// item 2; A/B builds only, -DDQDK_CEIL=1 or 2; the table comes out empty):
+// the same phase A, load ring, windows, checksum sums and key arithmetic,
+// but no LDS stage, no round flush and no round barrier.  A window's two
+// keys (as fused_pair computes them) are packed to 16 bits each and the
+// wave writes them with one streaming store per window to a region of its
+// own: 256 contiguous bytes a window, against the shipped decode's 243 B of
+// key triples per 1500 B frame (91 events x 8/3 B) written through the
+// stage.  DQDK_CEIL=2 issues the same stores to an offset past the region
+// (dropped: the arithmetic stays live, nothing is written).
+__device__ __forceinline__ uint32_t ceil_keys(const u32x4& va, const u32x4& vb, uint32_t r, uint32_t e0, uint32_t Ef)
+{
+    uint32_t out = 0;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const u32x4& v = c ? vb : va;
+        const uint32_t x = __builtin_amdgcn_alignbyte(v.y, v.x, r);
+        const uint32_t y = __builtin_amdgcn_alignbyte(v.z, v.y, r);
+        const uint32_t ch = x & 0xffffu;
+        const uint32_t bin = __builtin_amdgcn_perm(y, x, 0x0c0c0403u);
+        const uint32_t hc = __builtin_amdgcn_ubfe(y, 16, 3);
+        const uint32_t key = __umul24(ch, kHists << 16) + (hc << 16) + bin;
+        const bool ink = e0 + 64u * c < Ef && ch < kChannels && hc < kHists;
+        out |= (ink ? (key ^ (key >> 16)) & 0xffffu : 0u) << (16 * c);
+    }
+    return out;
+}
+#endif
+
 // Phase A's keys (akey[0, na), KEY_NONE: out of bounds) into the stage, as
 // fused_pair stages a window's: every returning LDS add first (lanes with
 // no key add to their sink word), one wait, then the stores, then one
@@ -1419,6 +1452,14 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     const int W = (int)a.round_windows;
     uint32_t fcur = 0;  // the piece cursor of this lane's bucket (wave + kFWaves * lane)
     int kr = 0;         // windows of the current round so far: rounds run on across super-tiles
+#if DQDK_CEIL
+    // the ceiling's per-wave output region (1 KiB-aligned share of the pieces' allocation)
+    const uint64_t ceil_words =
+        ((uint64_t)kL1Buckets * a.region / ((uint64_t)gridDim.x * kFWaves)) & ~(uint64_t)255;
+    const __amdgpu_buffer_rsrc_t ceil_rsrc =
+        uniform_rsrc(a.part1 + ((uint64_t)blockIdx.x * kFWaves + wave) * ceil_words, ceil_words * 4u);
+    uint32_t ceil_off = (uint32_t)lane * 4u;
+#endif
     for (uint32_t st = blockIdx.x; st < nsuper; st += gridDim.x) {
         const uint32_t tile = st * kFWaves + wave;
         // frame of this lane: tile-major (64 consecutive frames per wave), or
@@ -1523,7 +1564,16 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 }
                 const uint32_t Ef = active ? P.Ef : 0u;
                 const uint32_t e0 = jw + (uint32_t)lane - P.de;
+#if DQDK_CEIL
+                {
+                    const uint32_t cw = ceil_keys(b0[d], b1[d], P.r, e0, Ef);
+                    __builtin_amdgcn_raw_buffer_store_b32(cw, ceil_rsrc, DQDK_CEIL == 1 && active ? ceil_off : kOOB,
+                                                          0, kFstAuxLines);
+                    ceil_off += active ? 256u : 0u;
+                }
+#else
                 fused_pair(a, b0[d], b1[d], P.r, e0, Ef, wslot0 + jp, lds, ovf_rsrc, (uint32_t)lane);
+#endif
                 if (active && ++wp == P.nwin) {
                     frame_sum_add(&lds.sum[wslot0 + jp], &lds.csink[lane], acc0 + acc1,
                                   (lane & 15) == 15);
@@ -1538,7 +1588,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
                 issue(b0[d], b1[d]);
             }
             kr += kFRingW;
-            if (kr == W) {  // end of a round (block-uniform)
+            if (!DQDK_CEIL && kr == W) {  // end of a round (block-uniform)
                 kr = 0;
                 lds_barrier();
                 fused_flush<kLines, false>(a, lds, lane, wave, fcur, ovf_rsrc);
@@ -1560,7 +1610,8 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
     }
     // the keys still staged, then the piece sizes for rx_part1 / rx_part2
     lds_barrier();
-    fused_flush<kLines, true>(a, lds, lane, wave, fcur, ovf_rsrc);
+    if (!DQDK_CEIL)
+        fused_flush<kLines, true>(a, lds, lane, wave, fcur, ovf_rsrc);
     {
         const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
         if (b < (uint32_t)kL1Buckets)

@@ -76,16 +76,26 @@ class RxQueue:
 
     # -- lifecycle ---------------------------------------------------------
     def close(self) -> None:
+        """Destroy the queue; raises DqdkError when its last work or its
+        teardown failed (a device fault is reported here, by the queue that
+        ran the work, not by a later call)."""
         if getattr(self, "_h", None):
-            L.lib().dqdk_gpu_queue_destroy(self._h)
+            rc = L.lib().dqdk_gpu_queue_destroy(self._h)
             self._h = None
             self._pinned = {}
+            L.check(rc, "dqdk_gpu_queue_destroy")
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
-        self.close()
+        if exc[0] is None:
+            self.close()
+        else:  # the body's exception is the one reported
+            try:
+                self.close()
+            except L.DqdkError:
+                pass
 
     def __del__(self):
         try:
@@ -128,7 +138,7 @@ class RxQueue:
         n = len(desc)
         res = np.zeros(n, dtype=L.RESULT_DTYPE)
         delta = L.Counters()
-        self._keep(umem)  # (registered on first use)
+        self._keep(umem)  # (registered on first use: held while registered)
         L.check(L.lib().dqdk_gpu_rx_batch(self._h, umem.ctypes.data, umem.nbytes, desc.ctypes.data, n,
                                           res.ctypes.data, C.byref(delta)), "dqdk_gpu_rx_batch")
         return res, delta.as_dict()
@@ -168,10 +178,16 @@ class RxQueue:
         self._keep(umem)
 
     def _keep(self, umem: np.ndarray) -> None:
-        """Hold the largest buffer seen at the address (a view keeps its base)."""
-        cur = self._pinned.get(umem.ctypes.data)
-        if cur is None or cur.nbytes < umem.nbytes:
-            self._pinned[umem.ctypes.data] = umem
+        """Hold a buffer the C side registers for it (dqdk_gpu_umem_register's
+        rules): nothing when a held registration already covers it (a view
+        inside a registered UMEM creates none), else the buffer, replacing a
+        smaller one at the same address (the C side replaces that
+        registration too).  Held until unregistered or the queue closes."""
+        a, n = umem.ctypes.data, umem.nbytes
+        for base, buf in self._pinned.items():
+            if base <= a and a + n <= base + buf.nbytes:
+                return
+        self._pinned[a] = umem
 
     def unregister_umem(self, umem: np.ndarray) -> None:
         L.check(L.lib().dqdk_gpu_umem_unregister(self._h, umem.ctypes.data), "umem_unregister")
@@ -364,8 +380,9 @@ class DeviceBuffer:
 
     def close(self) -> None:
         if self.ptr:
-            L.lib().dqdk_gpu_device_free(self.device, self.ptr)
+            rc = L.lib().dqdk_gpu_device_free(self.device, self.ptr)
             self.ptr = 0
+            L.check(rc, "dqdk_gpu_device_free")
 
     def __enter__(self):
         return self

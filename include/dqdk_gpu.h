@@ -149,6 +149,10 @@ int dqdk_gpu_device_count(void);
  * batches too small to partition) adds n * E * 8 B (keys + their grouped copy)
  * on its first batch -- allocated at creation when the flags force it. */
 int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_batch, dqdk_gpu_queue_t** out);
+/* destroy waits for the queue's work, releases everything it holds whatever
+ * fails, and returns 0 or the first failure (-EIO, dqdk_gpu_last_error names
+ * the call): a device fault left by the queue's last kernels or copies is
+ * reported by the destroy, not by the caller's next HIP call. */
 int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q);
 /* Queues start on a stream of their own (hipStreamNonBlocking).  Run the
  * queue's work on the caller's hipStream_t instead -- verbatim, so NULL is
@@ -194,7 +198,11 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
  * dqdk_gpu_umem_register is a no-op for an address already registered with
  * at least `size` bytes; with fewer, the old registration is replaced (the
  * queue's stream drained first).  rx_batch registers a UMEM no registration
- * covers. */
+ * covers.  A registered UMEM must be unregistered (or its queue destroyed)
+ * BEFORE its memory is freed or unmapped: a registration outlives nothing it
+ * maps, and a new buffer placed at a freed one's address would otherwise be
+ * read through the old registration's pages (the reference's UMEM lives
+ * for the worker's lifetime, src/dqdk.c:109-127, so this is its order too). */
 int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size);
 int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
 int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,

@@ -479,13 +479,17 @@ int main(int argc, char** argv)
                lat[(nlat * 99) / 100], lat[nlat - 1]);
     }
     free(lat);
+    int bad = 0;
     for (int k = 0; k < nworkers; k++) {
         if (!fp) {
-            dqdk_gpu_umem_unregister(w[k].q, umem);
-            dqdk_gpu_queue_destroy(w[k].q);
+            /* a UMEM is unregistered before it is freed (include/dqdk_gpu.h) */
+            if (dqdk_gpu_umem_unregister(w[k].q, umem) || dqdk_gpu_queue_destroy(w[k].q)) {
+                fprintf(stderr, "teardown: %s\n", dqdk_gpu_last_error());
+                bad = 1;
+            }
         }
     }
     munlock(umem, size);
     munmap(umem, size);
-    return 0;
+    return bad;
 }

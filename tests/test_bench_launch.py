@@ -33,6 +33,18 @@ def test_gpus_n_spawns_n_ranks_and_aggregates():
     # rank 1 sleeps twice as long per step: the job time is the slowest rank's
     assert d["per_gpu"][1]["Mpkt_s"] < d["per_gpu"][0]["Mpkt_s"]
     assert abs(d["value"] - 2 * d["per_gpu"][1]["Mpkt_s"]) / d["value"] < 0.35
+    # every rank describes itself: its roofline kernel's
+    # time and fraction, its staging-probe outcome, its GPU
+    for r in d["per_gpu"]:
+        for k in ("decode_ms", "decode_alg_bytes", "decode_frac", "staging_probe", "bdf"):
+            assert k in r, (k, r)
+        assert "chosen" in r["staging_probe"] and "ns_per_frame" in r["staging_probe"]
+    agg = d["roofline_all_gpus"]
+    # sum of the ranks' bytes over the slowest rank's time, against N x 8 TB/s
+    alg = sum(r["decode_alg_bytes"] for r in d["per_gpu"])
+    t = max(r["decode_ms"] for r in d["per_gpu"]) * 1e-3
+    assert agg["peak"] == 2 * 8000.0 and abs(agg["frac"] - alg / t / 1e9 / 16000.0) < 1e-3
+    assert agg["slowest_rank"] == 1 and agg["min_rank_frac"] == d["per_gpu"][1]["decode_frac"]
 
 
 def test_default_is_one_rank():

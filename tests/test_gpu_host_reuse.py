@@ -1,0 +1,118 @@
+"""Host UMEM registration, then the same address reused by a new buffer.
+
+VERDICT r5 item 1 / ADVICE r5: four -m gpu runs (r04b, r04d, r05h, r05ac)
+stopped with hipErrorIllegalAddress at a test's FIRST pageable host-to-device
+copy.  In r05ac the test before was `test_small_batches_single_launch[256-4]`:
+a 1 MiB host UMEM (a numpy array: an mmap'd malloc chunk, data 16 B into
+its first page) copied to the device by torch, registered by the host
+drop-in (`dqdk_gpu_rx_batch` -> hipHostRegister), unregistered, the queue
+destroyed, the array freed (munmap); the faulting copy then read a fresh
+1,144,352-B array, which can sit at the same address.
+
+This runs exactly that ordering with the address reuse forced (the second
+buffer is mapped at the first one's address, MAP_FIXED_NOREPLACE), for the
+same, a larger and a smaller second buffer, with and without the pageable
+copy before the registration, and with the registration dropped by
+unregister or by the queue's destroy.  The ownership rule it rests on is the
+reference's: frames are valid until the descriptors are released
+(src/dqdk.c:300) and the UMEM lives as long as its worker (src/dqdk.c:109-127).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import dqdk_amd as D
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+_libc = C.CDLL(None, use_errno=True)
+_libc.mmap.restype = C.c_void_p
+_libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+_libc.munmap.restype = C.c_int
+_libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+PROT_RW = 0x1 | 0x2
+MAP_PRIVATE, MAP_ANONYMOUS, MAP_FIXED_NOREPLACE = 0x02, 0x20, 0x100000
+OFF = 16  # glibc's mmap'd chunks hand out memory 16 B into the first page
+PAGE = 4096
+
+
+def _span(nbytes: int) -> int:
+    return (OFF + nbytes + PAGE - 1) // PAGE * PAGE
+
+
+def _map(nbytes: int, at: int = 0) -> int:
+    flags = MAP_PRIVATE | MAP_ANONYMOUS | (MAP_FIXED_NOREPLACE if at else 0)
+    p = _libc.mmap(at or None, _span(nbytes), PROT_RW, flags, -1, 0)
+    if p is None or p == C.c_void_p(-1).value:
+        raise OSError(C.get_errno(), "mmap")
+    return p
+
+
+def _view(base: int, nbytes: int) -> np.ndarray:
+    return np.frombuffer((C.c_uint8 * nbytes).from_address(base + OFF), dtype=np.uint8)
+
+
+def _need_gpu():
+    if not torch.cuda.is_available() or D.device_count() < 1:
+        pytest.fail("GPU tests need a gfx950 device (none visible)")
+
+
+@pytest.mark.parametrize("unreg", ["unregister", "destroy"])
+@pytest.mark.parametrize("pre_copy", [True, False])
+@pytest.mark.parametrize("second", [1_048_576, 1_144_352, 524_288])
+def test_registered_umem_freed_then_address_reused_by_pageable_copy(second, pre_copy, unreg):
+    _need_gpu()
+    n = 256
+    c = D.rx.synth_cfg(1500, 4096, faulty=True)
+    first_len = (int(D._lib.lib().dqdk_synth_umem_size(C.byref(c), n)) + 15) // 16 * 16
+    a = _map(first_len)
+    umem = _view(a, first_len)
+    _, desc = D.synth_umem(n, 1500, 4096, faulty=True, first=7 * n, out=umem)
+    if pre_copy:  # as compare() does before the host drop-in
+        d = torch.from_numpy(umem).to("cuda:0")
+        torch.cuda.synchronize()
+        assert bool((d.cpu().numpy() == umem).all())
+        del d
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_PREFILTER | D.F_HISTO_ATOMIC, port_start=5000, port_end=5000)
+    q = D.RxQueue(0, cfg, 256)
+    q.enable_timing(True)
+    res, delta = q.process_batch(umem, desc)
+    q.read_timing()
+    ores, ocnt, _ = O.rx_batch(umem.copy(), desc, cfg.payloadsz, cfg.mode, cfg.flags, cfg.port_start, cfg.port_end)
+    np.testing.assert_array_equal(res, ores)
+    assert delta["rcvd_pkts"] == ocnt["rcvd_pkts"]
+    if unreg == "unregister":
+        q.unregister_umem(umem)
+    q.close()  # raises on any failure of the queue's work or teardown
+    torch.cuda.synchronize()
+    del umem
+    assert _libc.munmap(a, _span(first_len)) == 0
+
+    b = _map(second, at=a)  # the freed buffer's address, forced
+    assert b == a
+    try:
+        fresh = _view(b, second)
+        fresh[:] = np.random.default_rng(second).integers(0, 256, second, dtype=np.uint8)
+        d = torch.from_numpy(fresh).to("cuda:0")  # the copy r05ac faulted in
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d.cpu().numpy(), fresh)
+        del d, fresh
+    finally:
+        torch.cuda.synchronize()
+        _libc.munmap(b, _span(second))
+
+
+def test_destroy_reports_success_and_device_free_checks():
+    """destroy and device_free return their calls' results (0 here); a
+    double destroy is impossible through the Python queue (closed once)."""
+    _need_gpu()
+    q = D.RxQueue(0, D.RxConfig(payloadsz=1458), 1024)
+    q.close()
+    q.close()  # no-op
+    buf = D.DeviceBuffer(0, 1 << 20)
+    buf.close()
+    buf.close()  # no-op
