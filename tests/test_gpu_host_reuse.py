@@ -44,9 +44,9 @@ def _span(nbytes: int) -> int:
     return (OFF + nbytes + PAGE - 1) // PAGE * PAGE
 
 
-def _map(nbytes: int, at: int = 0) -> int:
+def _map(nbytes: int, at: int = 0, span: int = 0) -> int:
     flags = MAP_PRIVATE | MAP_ANONYMOUS | (MAP_FIXED_NOREPLACE if at else 0)
-    p = _libc.mmap(at or None, _span(nbytes), PROT_RW, flags, -1, 0)
+    p = _libc.mmap(at or None, span or _span(nbytes), PROT_RW, flags, -1, 0)
     if p is None or p == C.c_void_p(-1).value:
         raise OSError(C.get_errno(), "mmap")
     return p
@@ -69,7 +69,8 @@ def test_registered_umem_freed_then_address_reused_by_pageable_copy(second, pre_
     n = 256
     c = D.rx.synth_cfg(1500, 4096, faulty=True)
     first_len = (int(D._lib.lib().dqdk_synth_umem_size(C.byref(c), n)) + 15) // 16 * 16
-    a = _map(first_len)
+    span = max(_span(first_len), _span(second))  # (room for the larger second buffer at the same address)
+    a = _map(first_len, span=span)
     umem = _view(a, first_len)
     _, desc = D.synth_umem(n, 1500, 4096, faulty=True, first=7 * n, out=umem)
     if pre_copy:  # as compare() does before the host drop-in
@@ -90,7 +91,7 @@ def test_registered_umem_freed_then_address_reused_by_pageable_copy(second, pre_
     q.close()  # raises on any failure of the queue's work or teardown
     torch.cuda.synchronize()
     del umem
-    assert _libc.munmap(a, _span(first_len)) == 0
+    assert _libc.munmap(a, span) == 0
 
     b = _map(second, at=a)  # the freed buffer's address, forced
     assert b == a
