@@ -7,6 +7,7 @@ Expected CSV text is produced here with the reference's own format strings
 histogram of the same batch, so the file must match byte for byte.
 """
 import ctypes as C
+import errno
 import os
 
 import numpy as np
@@ -339,7 +340,11 @@ def test_raw_stream_failed_write_finishes_the_batch_first():
         with pytest.raises(D.DqdkError):
             q.set_raw_fd(-1)  # draining batch 1 into the broken pipe fails too
     finally:
-        q.close()
+        # batch 1's stream is still unwritten: destroy drains again and
+        # reports that failure too (include/dqdk_gpu.h)
+        with pytest.raises(D.DqdkError) as e:
+            q.close()
+        assert e.value.errno == errno.EPIPE
         os.close(w)
 
 
@@ -454,7 +459,12 @@ def test_destroy_with_deferred_raw_copy_in_flight_then_new_queue(tmp_path, broke
             except D.DqdkError:
                 assert broken and b == 1  # batch 0's deferred write() into the broken pipe
             q.unregister_umem(umem)
-        q.close()  # batch 1's copy may still be in flight here
+        if broken:  # destroy still drains: batch 1's write() fails, and destroy returns that failure
+            with pytest.raises(D.DqdkError) as ei:
+                q.close()  # batch 1's copy may still be in flight here
+            assert ei.value.errno == errno.EPIPE and "raw" in str(ei.value)
+        else:
+            q.close()  # batch 1's copy may still be in flight here
     finally:
         os.close(fd)
     # the next queue's first batch, on fresh allocations
