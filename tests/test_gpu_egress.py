@@ -340,11 +340,7 @@ def test_raw_stream_failed_write_finishes_the_batch_first():
         with pytest.raises(D.DqdkError):
             q.set_raw_fd(-1)  # draining batch 1 into the broken pipe fails too
     finally:
-        # batch 1's stream is still unwritten: destroy drains again and
-        # reports that failure too (include/dqdk_gpu.h)
-        with pytest.raises(D.DqdkError) as e:
-            q.close()
-        assert e.value.errno == errno.EPIPE
+        q.close()  # (batch 1's failed write was reported by set_raw_fd: nothing pending)
         os.close(w)
 
 
