@@ -782,6 +782,14 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         StageTimer t(q, kStDecode);
         hipLaunchKernelGGL(rx_small_kernel, dim3(1), dim3(kTile), 0, q->stream, ra, ca);
     } else {
+        // per-packet counters folded into the decode, as on the fused path
+        // (not under batch-abort accounting, which needs the batch's first
+        // failure before it counts; not for the host drop-in's publishing
+        // batches, whose rx_count writes the pinned results)
+        ra.fold = !q->publish && !q->fold_off && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT);
+        ra.blk_cnt = q->d_blkcnt;
+        ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
+        ra.cum = q->d_cum;
         const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
 #define DQDK_DEC_BLOCKS_PER_CU 16u
@@ -792,7 +800,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     }
     HIPCHK(hipGetLastError());
 
-    if (fused ? !ra.fold : (n > (uint32_t)kTile || q->small_off)) {
+    if (!ra.fold && (fused || n > (uint32_t)kTile || q->small_off)) {
         const uint32_t grid_cnt = std::min<uint32_t>((n + 255) / 256, (uint32_t)q->cu_count * 4u);
         {
             StageTimer t(q, kStAbort);

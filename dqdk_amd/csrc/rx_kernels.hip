@@ -509,6 +509,7 @@ struct DecodeLds {
     uint32_t sum[kWaves * 64];   // checksum word sums per frame
     uint32_t sink[64];           // per-lane dump word (frame_sum_add)
     u32x4 tail[kWaves * 64];     // last checksum chunk per frame (tail correction)
+    alignas(8) uint32_t fc[kFoldWords];  // folded counters of the block (RxArgs::fold; FoldWord)
 };
 
 // Per-frame stream parameters in the owning lane's VGPRs.
@@ -775,6 +776,113 @@ __device__ __forceinline__ void phase_c(const RxArgs& a, uint32_t i, bool live, 
     }
 }
 
+// Folded counters (RxArgs::fold): the block's sums of rx_count's per-frame
+// accounting (src/dqdk.c:252-322 per-packet form), in LDS then blk_cnt.
+enum FoldWord { F_FILT, F_FRAMES, F_IP, F_UDP, F_EMPTY, F_OK, F_BYTES_LO, F_BYTES_HI, F_OOB, F_FAIL, F_NWORDS };
+
+// One wave's frames of a super-tile into the block's folded counters
+// (ballots and DPP sums; lane 0 adds to LDS).  i: the lane's frame index.
+__device__ __forceinline__ void fold_frames(const RxArgs& a, uint32_t* fc, bool live, const dqdk_gpu_rx_result_t& r,
+                                            uint32_t i, int lane)
+{
+    const uint32_t st = r.status;
+    const bool inb = st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
+    const bool ok = live && st == DQDK_RX_OK;
+    const bool fail = live && inb && st != DQDK_RX_OK;
+    const uint64_t mfail = __ballot(fail);
+    uint32_t ifail = fail ? i : ~0u;  // the wave's first failing frame
+    if (mfail) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            ifail = min(ifail, (uint32_t)__shfl_xor((int)ifail, o));
+    }
+    const uint32_t filt = (uint32_t)__builtin_popcountll(__ballot(live && !inb));
+    const uint32_t frames = (uint32_t)__builtin_popcountll(__ballot(live && inb));
+    const uint32_t ip = (uint32_t)__builtin_popcountll(
+        __ballot(live && (st == DQDK_RX_INVALID_IP || st == DQDK_RX_INVALID_IP_CSUM)));
+    const uint32_t udp = (uint32_t)__builtin_popcountll(
+        __ballot(live && (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM)));
+    const uint32_t empty = (uint32_t)__builtin_popcountll(__ballot(live && st == DQDK_RX_EMPTY));
+    const uint32_t nok = (uint32_t)__builtin_popcountll(__ballot(ok));
+    // datalen is a u32 that wraps to ~4 G for udplen < 8 (dqdk.c:205): the
+    // wave sums its 16-bit halves (64 x 65535 < 2^32 each)
+    const uint32_t dl = ok ? r.datalen : 0u;
+    const uint64_t bytes = (uint64_t)wave_sum_dpp(dl & 0xffffu) + ((uint64_t)wave_sum_dpp(dl >> 16) << 16);
+    const uint32_t oob = wave_sum_dpp(ok && a.histo ? (uint32_t)r.oob_events : 0u);
+    if (lane == 0) {
+        if (filt)
+            atomicAdd(&fc[F_FILT], filt);
+        if (frames)
+            atomicAdd(&fc[F_FRAMES], frames);
+        if (ip)
+            atomicAdd(&fc[F_IP], ip);
+        if (udp)
+            atomicAdd(&fc[F_UDP], udp);
+        if (empty)
+            atomicAdd(&fc[F_EMPTY], empty);
+        if (nok)
+            atomicAdd(&fc[F_OK], nok);
+        if (bytes)
+            atomicAdd((unsigned long long*)&fc[F_BYTES_LO], (unsigned long long)bytes);  // (u64 per block)
+        if (oob)
+            atomicAdd(&fc[F_OOB], oob);
+        if (mfail)
+            atomicMin(&fc[F_FAIL], ifail);
+    }
+}
+
+// The block's folded counters into the batch's accumulators (a.blk_cnt as
+// u64 words: device atomics, which execute at the memory side, so no fence
+// and no L2 write-back -- an agent-scope fence here wrote back every XCD's
+// dirty piece lines under the still-running blocks: decode +0.1 ms); the
+// last block (ticket, taken once its own adds have returned) swaps the
+// totals out, resetting them, and publishes the batch: batch_scratch [0] =
+// first failing frame (n: none), [1..12] = dqdk_gpu_counters_t of the batch,
+// each added to cum -- what rx_abort + rx_count write for a per-packet batch.
+__device__ __forceinline__ void fold_publish(const RxArgs& a, uint32_t* fc, int tid)
+{
+    __shared__ uint32_t last;
+    __shared__ uint64_t tot[F_NWORDS];
+    unsigned long long* acc = (unsigned long long*)a.blk_cnt;  // [F_NWORDS] (F_BYTES_HI unused)
+    __syncthreads();  // every wave's fold_frames adds are in LDS
+    if (tid < 64) {
+        uint64_t r = 0;
+        if (tid < F_NWORDS && tid != F_BYTES_HI) {
+            const uint64_t v = tid == F_BYTES_LO ? *(const uint64_t*)&fc[F_BYTES_LO] : (uint64_t)fc[tid];
+            r = tid == F_FAIL ? atomicMin(&acc[F_FAIL], (unsigned long long)v) : atomicAdd(&acc[tid], (unsigned long long)v);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(r) : "memory");  // the adds are performed before the ticket
+        if (tid == 0)
+            last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last)
+        return;  // (block-uniform)
+    if (tid < F_NWORDS && tid != F_BYTES_HI)
+        tot[tid] = atomicExch(&acc[tid], tid == F_FAIL ? ~0ull : 0ull);  // the totals; reset for the next batch
+    __syncthreads();
+    if (tid == 0) {
+        const uint64_t n = a.n;
+        const uint64_t fail = tot[F_FAIL] < n ? tot[F_FAIL] : n;
+        const uint64_t c[12] = {tot[F_FRAMES], tot[F_FRAMES], tot[F_BYTES_LO], tot[F_IP],
+                                tot[F_UDP],    fail < n ? 1ull : 0ull, tot[F_OK] * a.E, tot[F_BYTES_LO],
+                                tot[F_OOB],    tot[F_EMPTY], tot[F_FILT], fail};
+        unsigned long long* cum = (unsigned long long*)a.cum;
+        a.batch_scratch[0] = fail;
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            a.batch_scratch[1 + k] = c[k];
+            if (k < 11 && c[k])
+                atomicAdd(&cum[k], (unsigned long long)c[k]);
+        }
+        cum[11] = fail;  // first_abort_idx of this batch
+#pragma unroll
+        for (int k = 1 + 12; k < 17; k++)  // (the rest of the per-batch words the unfolded decode resets)
+            a.batch_scratch[k] = 0;
+        *a.ticket = 0;
+    }
+}
+
 __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile, uint32_t F, int lane,
                                                  uint32_t wave, DecodeLds& lds)
 {
@@ -863,6 +971,8 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     lds.sum[my] = 0;
     lds.cnt[kLdsOob + my] = 0;
     phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, lds.tail[my]);
+    if (a.fold)  // per-packet counters summed here: no rx_abort / rx_count launches
+        fold_frames(a, lds.fc, live, r, i, lane);
     // the partitioned histogram reads records by index only: every non-OK
     // frame gets KEY_NONE records (rare; after this wave's speculative stores)
     const bool fill = live && a.cnt1 && a.keys && a.E && r.status != DQDK_RX_OK;
@@ -884,9 +994,13 @@ __device__ __forceinline__ void decode_block(const RxArgs& a, DecodeLds& lds)
     for (int b = tid; b < kLdsCnt; b += kTile)
         lds.cnt[b] = 0;
     lds.sum[tid] = 0;
+    if (tid < kFoldWords)
+        lds.fc[tid] = tid == F_FAIL ? ~0u : 0u;
     __syncthreads();
-    if (blockIdx.x == 0 && tid < 17)
-        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;  // per-batch state reset
+    // per-batch state reset (folded counters: the last block's fold_publish
+    // writes these words instead)
+    if (!a.fold && blockIdx.x == 0 && tid < 17)
+        a.batch_scratch[tid] = tid == 0 ? (uint64_t)a.n : 0ull;
 
     const uint32_t F = a.tile_frames ? a.tile_frames : 64u;
     const uint32_t ntiles = (a.n + F - 1) / F;
@@ -899,6 +1013,8 @@ __device__ __forceinline__ void decode_block(const RxArgs& a, DecodeLds& lds)
             if (lds.cnt[b])
                 atomicAdd(&a.cnt1[b], lds.cnt[b]);
     }
+    if (a.fold)
+        fold_publish(a, lds.fc, tid);
 }
 
 __global__ void __launch_bounds__(kTile) rx_decode_kernel(RxArgs a)
@@ -996,113 +1112,6 @@ struct FusedLds {
     uint32_t ovf_n;                  // keys in this block's private overflow region
     alignas(8) uint32_t fc[kFoldWords];  // folded counters of the block (FoldWord; the bytes word pair is a u64)
 };
-
-// Folded counters (RxArgs::fold): the block's sums of rx_count's per-frame
-// accounting (src/dqdk.c:252-322 per-packet form), in LDS then blk_cnt.
-enum FoldWord { F_FILT, F_FRAMES, F_IP, F_UDP, F_EMPTY, F_OK, F_BYTES_LO, F_BYTES_HI, F_OOB, F_FAIL, F_NWORDS };
-
-// One wave's frames of a super-tile into the block's folded counters
-// (ballots and DPP sums; lane 0 adds to LDS).  i: the lane's frame index.
-__device__ __forceinline__ void fold_frames(const RxArgs& a, FusedLds& lds, bool live, const dqdk_gpu_rx_result_t& r,
-                                            uint32_t i, int lane)
-{
-    const uint32_t st = r.status;
-    const bool inb = st != DQDK_RX_FILTER_DROP && st != DQDK_RX_FILTER_PASS;
-    const bool ok = live && st == DQDK_RX_OK;
-    const bool fail = live && inb && st != DQDK_RX_OK;
-    const uint64_t mfail = __ballot(fail);
-    uint32_t ifail = fail ? i : ~0u;  // the wave's first failing frame
-    if (mfail) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1)
-            ifail = min(ifail, (uint32_t)__shfl_xor((int)ifail, o));
-    }
-    const uint32_t filt = (uint32_t)__builtin_popcountll(__ballot(live && !inb));
-    const uint32_t frames = (uint32_t)__builtin_popcountll(__ballot(live && inb));
-    const uint32_t ip = (uint32_t)__builtin_popcountll(
-        __ballot(live && (st == DQDK_RX_INVALID_IP || st == DQDK_RX_INVALID_IP_CSUM)));
-    const uint32_t udp = (uint32_t)__builtin_popcountll(
-        __ballot(live && (st == DQDK_RX_INVALID_UDP || st == DQDK_RX_INVALID_UDP_CSUM)));
-    const uint32_t empty = (uint32_t)__builtin_popcountll(__ballot(live && st == DQDK_RX_EMPTY));
-    const uint32_t nok = (uint32_t)__builtin_popcountll(__ballot(ok));
-    // datalen is a u32 that wraps to ~4 G for udplen < 8 (dqdk.c:205): the
-    // wave sums its 16-bit halves (64 x 65535 < 2^32 each)
-    const uint32_t dl = ok ? r.datalen : 0u;
-    const uint64_t bytes = (uint64_t)wave_sum_dpp(dl & 0xffffu) + ((uint64_t)wave_sum_dpp(dl >> 16) << 16);
-    const uint32_t oob = wave_sum_dpp(ok && a.histo ? (uint32_t)r.oob_events : 0u);
-    if (lane == 0) {
-        if (filt)
-            atomicAdd(&lds.fc[F_FILT], filt);
-        if (frames)
-            atomicAdd(&lds.fc[F_FRAMES], frames);
-        if (ip)
-            atomicAdd(&lds.fc[F_IP], ip);
-        if (udp)
-            atomicAdd(&lds.fc[F_UDP], udp);
-        if (empty)
-            atomicAdd(&lds.fc[F_EMPTY], empty);
-        if (nok)
-            atomicAdd(&lds.fc[F_OK], nok);
-        if (bytes)
-            atomicAdd((unsigned long long*)&lds.fc[F_BYTES_LO], (unsigned long long)bytes);  // (u64 per block)
-        if (oob)
-            atomicAdd(&lds.fc[F_OOB], oob);
-        if (mfail)
-            atomicMin(&lds.fc[F_FAIL], ifail);
-    }
-}
-
-// The block's folded counters into the batch's accumulators (a.blk_cnt as
-// u64 words: device atomics, which execute at the memory side, so no fence
-// and no L2 write-back -- an agent-scope fence here wrote back every XCD's
-// dirty piece lines under the still-running blocks: decode +0.1 ms); the
-// last block (ticket, taken once its own adds have returned) swaps the
-// totals out, resetting them, and publishes the batch: batch_scratch [0] =
-// first failing frame (n: none), [1..12] = dqdk_gpu_counters_t of the batch,
-// each added to cum -- what rx_abort + rx_count write for a per-packet batch.
-__device__ __forceinline__ void fold_publish(const RxArgs& a, FusedLds& lds, int tid)
-{
-    __shared__ uint32_t last;
-    __shared__ uint64_t tot[F_NWORDS];
-    unsigned long long* acc = (unsigned long long*)a.blk_cnt;  // [F_NWORDS] (F_BYTES_HI unused)
-    __syncthreads();  // every wave's fold_frames adds are in LDS
-    if (tid < 64) {
-        uint64_t r = 0;
-        if (tid < F_NWORDS && tid != F_BYTES_HI) {
-            const uint64_t v = tid == F_BYTES_LO ? *(const uint64_t*)&lds.fc[F_BYTES_LO] : (uint64_t)lds.fc[tid];
-            r = tid == F_FAIL ? atomicMin(&acc[F_FAIL], (unsigned long long)v) : atomicAdd(&acc[tid], (unsigned long long)v);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::"v"(r) : "memory");  // the adds are performed before the ticket
-        if (tid == 0)
-            last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last)
-        return;  // (block-uniform)
-    if (tid < F_NWORDS && tid != F_BYTES_HI)
-        tot[tid] = atomicExch(&acc[tid], tid == F_FAIL ? ~0ull : 0ull);  // the totals; reset for the next batch
-    __syncthreads();
-    if (tid == 0) {
-        const uint64_t n = a.n;
-        const uint64_t fail = tot[F_FAIL] < n ? tot[F_FAIL] : n;
-        const uint64_t c[12] = {tot[F_FRAMES], tot[F_FRAMES], tot[F_BYTES_LO], tot[F_IP],
-                                tot[F_UDP],    fail < n ? 1ull : 0ull, tot[F_OK] * a.E, tot[F_BYTES_LO],
-                                tot[F_OOB],    tot[F_EMPTY], tot[F_FILT], fail};
-        unsigned long long* cum = (unsigned long long*)a.cum;
-        a.batch_scratch[0] = fail;
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            a.batch_scratch[1 + k] = c[k];
-            if (k < 11 && c[k])
-                atomicAdd(&cum[k], (unsigned long long)c[k]);
-        }
-        cum[11] = fail;  // first_abort_idx of this batch
-#pragma unroll
-        for (int k = 1 + 12; k < 17; k++)  // (the rest of the per-batch words the unfolded decode resets)
-            a.batch_scratch[k] = 0;
-        *a.ticket = 0;
-    }
-}
 
 // Block barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release + acquire: on gfx950 that is s_waitcnt vmcnt(0) before s_barrier,
@@ -1603,7 +1612,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         lds.oob[my] = 0;
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, u32x4{0u, 0u, 0u, 0u});
         if (a.fold)
-            fold_frames(a, lds, live, r, i, lane);
+            fold_frames(a, lds.fc, live, r, i, lane);
         // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
         if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
             a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
@@ -1637,7 +1646,7 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
             atomicAdd(&a.scratch[kOffCnt1 + tid], lds.scnt[tid]);
     }
     if (a.fold)
-        fold_publish(a, lds, tid);
+        fold_publish(a, lds.fc, tid);
 }
 
 // the shipped variants (fused_policy_default: 3 from 128 events per frame,

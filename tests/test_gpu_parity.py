@@ -391,12 +391,19 @@ def test_configs2_jumbo_full_batch_vs_oracle():
     assert np.array_equal(hist, table)
 
 
+@pytest.mark.parametrize("fold", [True, False], ids=["folded", "fold-off"])
 @pytest.mark.parametrize("hpath,kernels", [
-    (D.F_HISTO_ATOMIC, {"rx_decode", "rx_abort", "rx_count", "rx_histo_atomic"}),
-    (D.F_HISTO_PARTITIONED | D.F_HISTO_EAGER, {"rx_decode", "rx_abort", "rx_count", "rx_part1", "rx_part2",
-                             "rx_slice_histo"})], ids=["atomic", "partitioned"])
-def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels):
+    (D.F_HISTO_ATOMIC, {"rx_decode", "rx_histo_atomic"}),
+    (D.F_HISTO_PARTITIONED | D.F_HISTO_EAGER, {"rx_decode", "rx_part1", "rx_part2", "rx_slice_histo"})],
+    ids=["atomic", "partitioned"])
+def test_stage_timing_reports_every_kernel_once_per_batch(hpath, kernels, fold, monkeypatch):
+    """The records path's kernels, each timed once per batch: the per-packet
+    counters folded into rx_decode (default), or counted by rx_abort +
+    rx_count launches (DQDK_GPU_FOLD=0, read at queue creation)."""
     _need_gpu()
+    if not fold:
+        monkeypatch.setenv("DQDK_GPU_FOLD", "0")
+        kernels = kernels | {"rx_abort", "rx_count"}
     umem, desc = D.synth_umem(1024, 1500, 4096)
     cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | hpath)
     q = D.RxQueue(0, cfg, len(desc))
