@@ -301,7 +301,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
             qr.process_device(d_umem.data_ptr(), umem_bytes, d_desc.data_ptr(), n, d_res.data_ptr(),
                               d_keys.data_ptr())
             torch.cuda.synchronize(dev)
-    items = K // 15360 + 284 + 1  # part2 work items (15360-key chunks of the 284 buckets)
+    items = K // 18432 + 284 + 1  # part2 work items (18432-key chunks of the 284 buckets, rx_kernels.h kPartChunk)
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
     if histo and E:

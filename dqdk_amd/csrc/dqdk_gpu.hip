@@ -193,7 +193,7 @@ struct dqdk_gpu_queue {
     uint32_t* d_ovf = nullptr;     // fused path: the overflow list (ovf_blk_elems keys)
     uint32_t ovf_cap_blk = 0;      // fused path: keys per block overflow region
     uint16_t* d_part2 = nullptr;
-    uint16_t* d_runs = nullptr;    // part2 run offsets per 16K-key chunk
+    uint16_t* d_runs = nullptr;    // part2 run offsets per item (kPartChunk keys)
     uint32_t* d_hscratch = nullptr;
     // staged slots whose per-batch counters (scratch [0, kZeroWords)) are not
     // known to be zero: set until a batch's rx_part2 (which re-zeroes them
@@ -214,6 +214,7 @@ struct dqdk_gpu_queue {
     uint32_t fmap = 0;             // DQDK_GPU_FRAME_MAP=1: interleaved fused frame map
     bool p2zero_off = false;       // DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch
     bool small_off = false;        // DQDK_GPU_SMALL=0: small batches take the three-launch form too
+    uint32_t tile_frames = 0;      // DQDK_GPU_TILE_FRAMES: records-path decode frames per wave tile (0: 64)
     // Staging placement probe: the fused decode's rate
     // depends on where its piece buffer (d_part1, the decode's write stream)
     // lands physically relative to the image it reads -- 2.12 vs 2.35 ms at
@@ -504,7 +505,7 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
     const uint32_t grid_p = std::min<uint32_t>((uint32_t)((nkeys + kP1Chunk - 1) / kP1Chunk),
                                                (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
     const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
-                                                (uint32_t)q->cu_count * 2u);
+                                                (uint32_t)q->cu_count * (uint32_t)kP2BlocksPerCu);
     {
         // fused: the decode's piece scans and checksum-failed frames,
         // then the overflow list (usually empty), timed as "rx_fixup"
@@ -677,6 +678,8 @@ int read_knobs(dqdk_gpu_queue* q)
     q->fmap = env("DQDK_GPU_FRAME_MAP") ? (uint32_t)(atoi(env("DQDK_GPU_FRAME_MAP")) != 0) : 0u;
     q->p2zero_off = env("DQDK_GPU_P2ZERO") && !strcmp(env("DQDK_GPU_P2ZERO"), "0");
     q->small_off = env("DQDK_GPU_SMALL") && !strcmp(env("DQDK_GPU_SMALL"), "0");
+    if (const char* v = env("DQDK_GPU_TILE_FRAMES"))  // records-path decode: frames per wave tile (1-64)
+        q->tile_frames = std::min<uint32_t>(64, std::max<uint32_t>(1, (uint32_t)atoi(v)));
     q->probe = env("DQDK_GPU_STAGING_PROBE") && !strcmp(env("DQDK_GPU_STAGING_PROBE"), "0") ? 0 : 1;
     if (const char* v = env("DQDK_GPU_PIECE_SHIFT"))  // KiB (tools/state_probe.py)
         q->piece_shift = std::min<uint64_t>((uint64_t)atoll(v) * 256u, kPieceShiftMax - 256u) & ~63ull;
@@ -790,6 +793,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.blk_cnt = q->d_blkcnt;
         ra.ticket = (uint32_t*)(q->d_batch + kFoldTicketWord);
         ra.cum = q->d_cum;
+        ra.tile_frames = q->tile_frames;  // (0: 64-frame wave tiles)
         const uint32_t nblk = (n + kTile - 1) / kTile;
 #ifndef DQDK_DEC_BLOCKS_PER_CU
 #define DQDK_DEC_BLOCKS_PER_CU 16u

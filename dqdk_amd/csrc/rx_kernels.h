@@ -53,9 +53,21 @@ constexpr int kSliceBits = 14;                              // 2^14 bins per sli
 constexpr int kSubs = 1 << (kL1Shift - kSliceBits);         // 128 slices per bucket
 constexpr int kSlices = kL1Buckets * kSubs;                 // 36352 (36288 used)
 constexpr int kPartThreads = 1024;                          // part1/part2 block size
-constexpr int kPartKeysPerThread = 15;                      // five key triples per lane
-constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 15360 key slots staged in LDS (an item)
-constexpr int kPartTriples = kPartChunk / 3;                // 5120 triples: a gathered item
+#ifndef DQDK_P2_KPT
+#define DQDK_P2_KPT 18
+#endif
+constexpr int kPartKeysPerThread = DQDK_P2_KPT;             // six key triples per lane (r06d: 15 -> 18)
+static_assert(kPartKeysPerThread % 3 == 0, "a lane loads whole key triples");
+#ifndef DQDK_P2_PACKED
+#define DQDK_P2_PACKED 0
+#endif
+constexpr bool kP2Packed = DQDK_P2_PACKED;  // rx_part2: two u16 slice counters per LDS word (half the counter LDS)
+#ifndef DQDK_P2_BPC
+#define DQDK_P2_BPC 2
+#endif
+constexpr int kP2BlocksPerCu = DQDK_P2_BPC;                  // rx_part2 blocks per CU (its LDS allows two)
+constexpr int kPartChunk = kPartThreads * kPartKeysPerThread;  // 18432 key slots staged in LDS (an item)
+constexpr int kPartTriples = kPartChunk / 3;                // 6144 triples: a gathered item
 #ifndef DQDK_SLICE_SPAN
 #define DQDK_SLICE_SPAN 2
 #endif

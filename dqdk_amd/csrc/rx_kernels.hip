@@ -2067,8 +2067,8 @@ __global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArg
     }
 }
 
-// Level 2: each part2 item = one 16K-key chunk of a segment, sorted by slice
-// ((key >> 14) & 127) in LDS and written to part2 [item * 16K, + keys) as u16
+// Level 2: each part2 item = one kPartChunk-key chunk of a segment, sorted by slice
+// ((key >> 14) & 127) in LDS and written to part2 [item * kPartChunk, + keys) as u16
 // (the key's low 16 bits: readers mask off bits 14-15, the slice's), with the
 // run starts of its 128 slices.  A segment is a sequence of keys of one
 // L1 bucket: records path, rx_part1's run of the bucket; fused path, the
@@ -2103,16 +2103,21 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     constexpr int kMaxSeg = kL1Buckets * kSegsPerBucket;
     constexpr int kPWaves = kPartThreads / 64;
     constexpr int kJT = kPartKeysPerThread / 3;                      // triple loads per lane (gathered items)
-    constexpr uint32_t kWaveKeys = (uint32_t)kPartChunk / kPWaves;     // 960 key slots per wave
-    constexpr uint32_t kWaveTriples = kWaveKeys / 3;                  // 320 triple slots per wave
+    constexpr uint32_t kWaveKeys = (uint32_t)kPartChunk / kPWaves;     // 1152 key slots per wave
+    constexpr uint32_t kWaveTriples = kWaveKeys / 3;                  // 384 triple slots per wave
     constexpr uint32_t kDummy = 1u << kL1Shift;  // a slot past the item or a triple's pad (no stage slot)
-    constexpr int kCtr = kSubs * 32;             // counters: [slice][lane & 31]
-    static_assert(kCtr == 4 * kPartThreads, "the scan takes four counters per thread");
+    // counters: [slice][lane & 31]; packed (kP2Packed): two u16 counters a
+    // word, word [slice / 2][lane & 31], half slice % 2 -- the 32 lanes of a
+    // group still add to 32 different words, in half the LDS
+    constexpr int kCtr = kSubs * 32;
+    constexpr int kCtrW = kP2Packed ? kCtr / 2 : kCtr;  // counter words
+    static_assert(kCtrW == (kP2Packed ? 2 : 4) * kPartThreads, "the scan takes 4 (packed: 2 words of 2) counters a thread");
+    static_assert(!kP2Packed || 2 * kPartChunk + 2 < 65536, "packed cursors are u16 byte offsets");
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk + 2];  // + the dummies' sink
-    __shared__ __attribute__((aligned(16))) uint32_t cnt[kCtr];  // counts (x2: bytes), zero between items
-    __shared__ __attribute__((aligned(16))) uint32_t cur[kCtr];  // run cursors (byte offsets in the stage)
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[kCtrW];  // counts (x2: bytes), zero between items
+    __shared__ __attribute__((aligned(16))) uint32_t cur[kCtrW];  // run cursors (byte offsets in the stage)
     __shared__ uint32_t prt[2][kMaxFusedGrid + 1], prk[2][kMaxFusedGrid + 1];  // piece starts: triples, keys
-    __shared__ uint32_t s_cnt[kMaxSeg], s_base8[kMaxSeg], ist[kMaxSeg + 1];
+    __shared__ uint32_t s_cnt[kMaxSeg], ist[kMaxSeg + 1];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t wsum[kPWaves];
     const int tid = threadIdx.x;
@@ -2122,23 +2127,21 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
 
     // ---- prologue: segments (size, input index) and their first items ----
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
-    ((u32x4_t*)cnt)[tid] = u32x4_t{0u, 0u, 0u, 0u};
+    for (int w = tid; w < kCtrW; w += kPartThreads)
+        cnt[w] = 0u;
     __syncthreads();
     uint32_t nit = 0;
     if ((uint32_t)tid < nseg) {
         const uint32_t b = fused ? (uint32_t)tid >> 1 : (uint32_t)tid;
         uint32_t c, per;
-        uint64_t base = 0;
         if (!fused || (tid & 1)) {  // rx_part1's run of the bucket: keys
             c = a.scratch[kOffCur1 + b];
-            base = a.part1_base + off1[b];
             per = kPartChunk;
         } else {                    // the bucket's pieces: key triples
             c = a.scratch[kOffPiecePreT + b * (kMaxFusedGrid + 1) + a.fgrid];
             per = kPartTriples;
         }
         s_cnt[tid] = c;
-        s_base8[tid] = (uint32_t)(base / kBucketAlign);
         nit = (c + per - 1) / per;
     }
     const uint32_t incl = wave_incl_scan_dpp(nit);
@@ -2181,7 +2184,8 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         g.s0 = (item - rfl(ist[t])) * per;
         g.nu = min(rfl(s_cnt[t]) - g.s0, per);
         g.b = fused ? t >> 1 : t;
-        g.base8 = rfl(s_base8[t]) + g.s0 / kBucketAlign;
+        // (a contiguous run's input: rx_part1's run of the bucket, 8-key aligned)
+        g.base8 = g.gath ? 0u : (uint32_t)((a.part1_base + rfl(off1[g.b])) / kBucketAlign) + g.s0 / kBucketAlign;
         return g;
     };
     // a gathered item: its bucket's piece starts (then a barrier)
@@ -2209,9 +2213,9 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             prk[pb][t] = psk;
         }
     };
-    // slots: gathered items, wave w takes the item's triples [320w, 320w +
-    // 320), 64 per load (load j: triple 320w + 64j + lane -> keys 3j .. 3j + 2
-    // of the lane); contiguous items, keys [960w, 960w + 960), 64 per load
+    // slots: gathered items, wave w takes the item's triples [384w, 384w +
+    // 384), 64 per load (load j: triple 384w + 64j + lane -> keys 3j .. 3j + 2
+    // of the lane); contiguous items, keys [1152w, 1152w + 1152), 64 per load
     // (a gathered item's triple j loads into nk[2j], nk[2j + 1] and is
     // unpacked into key[3j .. 3j + 2] by count()).  A gathered item's loads
     // are issued a phase early: they land in nk while the previous item is
@@ -2323,20 +2327,70 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         const uint32_t sub4 = (lane & 31u) << 2;
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
-            // slice * 128 + (lane & 31) * 4: the counter's byte address
-            const uint32_t ca = ((key[j] >> (kSliceBits - 7)) & ((kSubs - 1) << 7)) | sub4;
+            // the counter's byte address: slice * 128 + (lane & 31) * 4, or
+            // packed (slice / 2) * 128 + (lane & 31) * 4 + (slice % 2) * 2
+            const uint32_t ca = kP2Packed ? ((key[j] >> (kSliceBits + 1 - 7)) & ((kSubs / 2 - 1) << 7)) | sub4 |
+                                                ((key[j] >> (kSliceBits - 1)) & 2u)
+                                          : ((key[j] >> (kSliceBits - 7)) & ((kSubs - 1) << 7)) | sub4;
             const uint32_t d = key[j] >> kL1Shift;  // 1: dummy
-            __hip_atomic_fetch_add(&cnt[ca >> 2], 2u - 2u * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t inc = (2u - 2u * d) << (kP2Packed ? (ca & 2u) << 3 : 0u);
+            __hip_atomic_fetch_add(&cnt[ca >> 2], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             key[j] = __builtin_amdgcn_perm(ca, key[j], 0x05040100u) | (d << 31);  // ca.lo16 : key.lo16
             // (opaque: scatter() re-derives the counter and increment from the
             // key; kept live across the scan they would spill)
             asm volatile("" : "+v"(key[j]));
         }
     };
+    // packed counters: thread t holds words 2t, 2t + 1 = slice pair p =
+    // t / 16 (one DPP row of 16 lanes a pair), lane slots 2 (t % 16) and + 1.
+    // Scan order is slice-major: the pair's low halves (slice 2p, lane slots
+    // 0..31), then its high halves (slice 2p + 1).  The block scan of every
+    // thread's low + high sums gives each pair's start; row scans of the
+    // low and the high sums give the offsets inside the pair.
+    auto scan_packed = [&](uint32_t item) -> uint32_t {
+        const u32x2 c = ((const u32x2*)cnt)[tid];
+        uint32_t z = 0;
+        asm volatile("" : "+v"(z));
+        ((u32x2*)cnt)[tid] = u32x2{z, z};
+        const uint32_t lo = (c.x & 0xffffu) + (c.y & 0xffffu), hi = (c.x >> 16) + (c.y >> 16);
+        const uint32_t sum = lo + hi;
+        const uint32_t incl = wave_incl_scan_dpp(sum);
+        uint32_t rlo = lo, rhi = hi;  // row (pair) inclusive scans
+        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x111, 0xf, 0xf, false);  // row_shr:1
+        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x111, 0xf, 0xf, false);
+        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x112, 0xf, 0xf, false);  // row_shr:2
+        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x112, 0xf, 0xf, false);
+        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x114, 0xf, 0xf, false);  // row_shr:4
+        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x114, 0xf, 0xf, false);
+        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x118, 0xf, 0xf, false);  // row_shr:8
+        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x118, 0xf, 0xf, false);
+        const uint32_t lotot = (uint32_t)__shfl((int)rlo, (int)(lane | 15u));  // the pair's low-half total
+        if (lane == 63)
+            wsum[wave] = incl;
+        lds_barrier();
+        const uint32_t x = lane < (uint32_t)kPWaves ? wsum[opaque(lane) & (kPWaves - 1)] : 0u;
+        const uint32_t woff = wave_sum_dpp(lane < wave ? x : 0u), tot = wave_sum_dpp(x);
+        const uint32_t exl = rlo - lo, exh = rhi - hi;     // inside the pair
+        const uint32_t ps = woff + incl - sum - exl - exh;  // the pair's start
+        const uint32_t l0 = ps + exl, h0 = ps + lotot + exh;
+        const uint32_t l1 = l0 + (c.x & 0xffffu), h1 = h0 + (c.x >> 16);
+        ((u32x2*)cur)[tid] = u32x2{l0 | (h0 << 16), l1 | (h1 << 16)};
+        uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
+        if ((lane & 15u) == 0) {
+            const uint32_t p2 = opaque((uint32_t)tid) >> 3;  // 2 p
+            ro[p2] = (uint16_t)(ps / 2);
+            ro[p2 + 1] = (uint16_t)((ps + lotot) / 2);
+        }
+        if (tid == 0)
+            ro[kSubs] = (uint16_t)(tot / 2);
+        return tot / 2;
+    };
     // scan: the counters (slice-major) into run cursors, four per thread;
     // the counts are zeroed for the next item.  Returns the item's valid
     // keys; item's 129 run starts (u16 offsets) go to runs.
     auto scan = [&](uint32_t item) -> uint32_t {
+        if constexpr (kP2Packed)
+            return scan_packed(item);
         const u32x4_t c = ((const u32x4_t*)cnt)[tid];
         uint32_t z = 0;
         asm volatile("" : "+v"(z));  // (a zero vector hoisted out of the item loop spills)
@@ -2372,9 +2426,14 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             uint32_t o[kSG];
 #pragma unroll
             for (int j = 0; j < kSG; j++)
-                if (h + j < kPartKeysPerThread)
-                    o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtr - 1)], 2u - 2u * (key[h + j] >> 31),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (h + j < kPartKeysPerThread) {
+                    const uint32_t sh = kP2Packed ? (key[h + j] >> 13) & 16u : 0u;  // packed: the half's shift
+                    o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtrW - 1)],
+                                                  (2u - 2u * (key[h + j] >> 31)) << sh, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (kP2Packed)
+                        o[j] = (o[j] >> sh) & 0xffffu;
+                }
 #pragma unroll
             for (int j = 0; j < kSG; j++)
                 if (h + j < kPartKeysPerThread)  // a dummy's u16 goes to the sink past the stage
