@@ -58,10 +58,6 @@ constexpr int kPartThreads = 1024;                          // part1/part2 block
 #endif
 constexpr int kPartKeysPerThread = DQDK_P2_KPT;             // six key triples per lane (r06d: 15 -> 18)
 static_assert(kPartKeysPerThread % 3 == 0, "a lane loads whole key triples");
-#ifndef DQDK_P2_PACKED
-#define DQDK_P2_PACKED 0
-#endif
-constexpr bool kP2Packed = DQDK_P2_PACKED;  // rx_part2: two u16 slice counters per LDS word (half the counter LDS)
 #ifndef DQDK_P2_BPC
 #define DQDK_P2_BPC 2
 #endif

@@ -2106,16 +2106,11 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
     constexpr uint32_t kWaveKeys = (uint32_t)kPartChunk / kPWaves;     // 1152 key slots per wave
     constexpr uint32_t kWaveTriples = kWaveKeys / 3;                  // 384 triple slots per wave
     constexpr uint32_t kDummy = 1u << kL1Shift;  // a slot past the item or a triple's pad (no stage slot)
-    // counters: [slice][lane & 31]; packed (kP2Packed): two u16 counters a
-    // word, word [slice / 2][lane & 31], half slice % 2 -- the 32 lanes of a
-    // group still add to 32 different words, in half the LDS
-    constexpr int kCtr = kSubs * 32;
-    constexpr int kCtrW = kP2Packed ? kCtr / 2 : kCtr;  // counter words
-    static_assert(kCtrW == (kP2Packed ? 2 : 4) * kPartThreads, "the scan takes 4 (packed: 2 words of 2) counters a thread");
-    static_assert(!kP2Packed || 2 * kPartChunk + 2 < 65536, "packed cursors are u16 byte offsets");
+    constexpr int kCtr = kSubs * 32;             // counters: [slice][lane & 31]
+    static_assert(kCtr == 4 * kPartThreads, "the scan takes four counters per thread");
     __shared__ __attribute__((aligned(16))) uint16_t stage[kPartChunk + 2];  // + the dummies' sink
-    __shared__ __attribute__((aligned(16))) uint32_t cnt[kCtrW];  // counts (x2: bytes), zero between items
-    __shared__ __attribute__((aligned(16))) uint32_t cur[kCtrW];  // run cursors (byte offsets in the stage)
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[kCtr];  // counts (x2: bytes), zero between items
+    __shared__ __attribute__((aligned(16))) uint32_t cur[kCtr];  // run cursors (byte offsets in the stage)
     __shared__ uint32_t prt[2][kMaxFusedGrid + 1], prk[2][kMaxFusedGrid + 1];  // piece starts: triples, keys
     __shared__ uint32_t s_cnt[kMaxSeg], ist[kMaxSeg + 1];
     __shared__ uint32_t off1[kL1Buckets + 1];
@@ -2127,8 +2122,7 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
 
     // ---- prologue: segments (size, input index) and their first items ----
     wave0_excl_scan(a.scratch + kOffCnt1, off1, kL1Buckets, true, kBucketAlign);
-    for (int w = tid; w < kCtrW; w += kPartThreads)
-        cnt[w] = 0u;
+    ((u32x4_t*)cnt)[tid] = u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
     uint32_t nit = 0;
     if ((uint32_t)tid < nseg) {
@@ -2327,70 +2321,20 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         const uint32_t sub4 = (lane & 31u) << 2;
 #pragma unroll
         for (int j = 0; j < kPartKeysPerThread; j++) {
-            // the counter's byte address: slice * 128 + (lane & 31) * 4, or
-            // packed (slice / 2) * 128 + (lane & 31) * 4 + (slice % 2) * 2
-            const uint32_t ca = kP2Packed ? ((key[j] >> (kSliceBits + 1 - 7)) & ((kSubs / 2 - 1) << 7)) | sub4 |
-                                                ((key[j] >> (kSliceBits - 1)) & 2u)
-                                          : ((key[j] >> (kSliceBits - 7)) & ((kSubs - 1) << 7)) | sub4;
+            // slice * 128 + (lane & 31) * 4: the counter's byte address
+            const uint32_t ca = ((key[j] >> (kSliceBits - 7)) & ((kSubs - 1) << 7)) | sub4;
             const uint32_t d = key[j] >> kL1Shift;  // 1: dummy
-            const uint32_t inc = (2u - 2u * d) << (kP2Packed ? (ca & 2u) << 3 : 0u);
-            __hip_atomic_fetch_add(&cnt[ca >> 2], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&cnt[ca >> 2], 2u - 2u * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             key[j] = __builtin_amdgcn_perm(ca, key[j], 0x05040100u) | (d << 31);  // ca.lo16 : key.lo16
             // (opaque: scatter() re-derives the counter and increment from the
             // key; kept live across the scan they would spill)
             asm volatile("" : "+v"(key[j]));
         }
     };
-    // packed counters: thread t holds words 2t, 2t + 1 = slice pair p =
-    // t / 16 (one DPP row of 16 lanes a pair), lane slots 2 (t % 16) and + 1.
-    // Scan order is slice-major: the pair's low halves (slice 2p, lane slots
-    // 0..31), then its high halves (slice 2p + 1).  The block scan of every
-    // thread's low + high sums gives each pair's start; row scans of the
-    // low and the high sums give the offsets inside the pair.
-    auto scan_packed = [&](uint32_t item) -> uint32_t {
-        const u32x2 c = ((const u32x2*)cnt)[tid];
-        uint32_t z = 0;
-        asm volatile("" : "+v"(z));
-        ((u32x2*)cnt)[tid] = u32x2{z, z};
-        const uint32_t lo = (c.x & 0xffffu) + (c.y & 0xffffu), hi = (c.x >> 16) + (c.y >> 16);
-        const uint32_t sum = lo + hi;
-        const uint32_t incl = wave_incl_scan_dpp(sum);
-        uint32_t rlo = lo, rhi = hi;  // row (pair) inclusive scans
-        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x111, 0xf, 0xf, false);  // row_shr:1
-        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x111, 0xf, 0xf, false);
-        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x112, 0xf, 0xf, false);  // row_shr:2
-        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x112, 0xf, 0xf, false);
-        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x114, 0xf, 0xf, false);  // row_shr:4
-        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x114, 0xf, 0xf, false);
-        rlo += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rlo, 0x118, 0xf, 0xf, false);  // row_shr:8
-        rhi += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rhi, 0x118, 0xf, 0xf, false);
-        const uint32_t lotot = (uint32_t)__shfl((int)rlo, (int)(lane | 15u));  // the pair's low-half total
-        if (lane == 63)
-            wsum[wave] = incl;
-        lds_barrier();
-        const uint32_t x = lane < (uint32_t)kPWaves ? wsum[opaque(lane) & (kPWaves - 1)] : 0u;
-        const uint32_t woff = wave_sum_dpp(lane < wave ? x : 0u), tot = wave_sum_dpp(x);
-        const uint32_t exl = rlo - lo, exh = rhi - hi;     // inside the pair
-        const uint32_t ps = woff + incl - sum - exl - exh;  // the pair's start
-        const uint32_t l0 = ps + exl, h0 = ps + lotot + exh;
-        const uint32_t l1 = l0 + (c.x & 0xffffu), h1 = h0 + (c.x >> 16);
-        ((u32x2*)cur)[tid] = u32x2{l0 | (h0 << 16), l1 | (h1 << 16)};
-        uint16_t* const ro = a.runs + (uint64_t)item * kItemOffs;
-        if ((lane & 15u) == 0) {
-            const uint32_t p2 = opaque((uint32_t)tid) >> 3;  // 2 p
-            ro[p2] = (uint16_t)(ps / 2);
-            ro[p2 + 1] = (uint16_t)((ps + lotot) / 2);
-        }
-        if (tid == 0)
-            ro[kSubs] = (uint16_t)(tot / 2);
-        return tot / 2;
-    };
     // scan: the counters (slice-major) into run cursors, four per thread;
     // the counts are zeroed for the next item.  Returns the item's valid
     // keys; item's 129 run starts (u16 offsets) go to runs.
     auto scan = [&](uint32_t item) -> uint32_t {
-        if constexpr (kP2Packed)
-            return scan_packed(item);
         const u32x4_t c = ((const u32x4_t*)cnt)[tid];
         uint32_t z = 0;
         asm volatile("" : "+v"(z));  // (a zero vector hoisted out of the item loop spills)
@@ -2426,14 +2370,9 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             uint32_t o[kSG];
 #pragma unroll
             for (int j = 0; j < kSG; j++)
-                if (h + j < kPartKeysPerThread) {
-                    const uint32_t sh = kP2Packed ? (key[h + j] >> 13) & 16u : 0u;  // packed: the half's shift
-                    o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtrW - 1)],
-                                                  (2u - 2u * (key[h + j] >> 31)) << sh, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (kP2Packed)
-                        o[j] = (o[j] >> sh) & 0xffffu;
-                }
+                if (h + j < kPartKeysPerThread)
+                    o[j] = __hip_atomic_fetch_add(&cur[(key[h + j] >> 18) & (kCtr - 1)], 2u - 2u * (key[h + j] >> 31),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
             for (int j = 0; j < kSG; j++)
                 if (h + j < kPartKeysPerThread)  // a dummy's u16 goes to the sink past the stage
@@ -2553,6 +2492,7 @@ struct SliceLds {
     uint32_t b_i0[kSliceMaxSlots], b_end[kSliceMaxSlots];  // the bucket's first item / inclusive prefix of its items per staged batch
     uint32_t w_tot[kSliceThreads / 64];
     uint32_t total;
+    uint32_t junk[64];  // DQDK_SLICE_TOUCH: the touches' LDS-DMA destination (never read)
 };
 constexpr uint32_t kDrainCap = 0xffffu - 0xffu;  // events per group: bins hold <= 255 after a drain
 
@@ -2773,6 +2713,33 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 }
             }
         };
+#ifndef DQDK_SLICE_TOUCH
+#define DQDK_SLICE_TOUCH 0
+#endif
+        // (A/B) the wave's next group's runs touched into L2 while this
+        // group is counted: one LDS-DMA dword per 128-B line (16 lanes an
+        // item; the destination is a junk word per lane, never read).  Inline
+        // asm, so hipcc's vmcnt bookkeeping does not see them: the group's own
+        // loads are waited for (a counted s_waitcnt) before they are issued,
+        // and the next group's loads, issued after them, retire after them.
+        auto touch = [&](uint32_t jn) {
+            const uint32_t q = min((uint32_t)lane >> 4, (uint32_t)kNI - 1u);
+            const uint32_t jj = jn + q * kWavesS;
+            const bool v = jj < nit;
+            if (!__ballot(v))
+                return;
+            const uint32_t jc = v ? jj : jn;
+            const uint32_t r = sl.s_run[jc < nit ? jc : 0u];
+            const uint32_t b0 = (2u * (r & 0xffffu)) & ~127u, b1 = 2u * (r >> 16);  // the run's bytes
+            uint32_t li = ((uint32_t)lane & 15u) * 128u;
+            li = b0 + li < b1 ? li : 0u;
+            const uint8_t* src = (const uint8_t*)(a.part2 + (uint64_t)sl.s_k[jc < nit ? jc : 0u] * a.part2_stride +
+                                                  (uint64_t)sl.s_base[jc < nit ? jc : 0u] * kPartChunk) + b0 + li;
+            const uint32_t dst = rfl((uint32_t)(uintptr_t)sl.junk);
+            uint32_t keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+        };
         for (uint32_t gs = 0; gs < nit;) {
             if (drains) {  // the group: the longest run of entries whose events fit kDrainCap - since
                 const uint32_t base = gs ? rfl(sl.s_pin[gs - 1]) : 0u, lim = kDrainCap - since;
@@ -2790,6 +2757,10 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             for (uint32_t j = gs + (uint32_t)wave; j < ge; j += kGrp) {
                 uint32_t w[kNI][kKG];
                 const uint32_t steps = issue(j, 0, w);
+                if (DQDK_SLICE_TOUCH) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this group's loads, known to hipcc
+                    touch(j + kGrp);
+                }
                 count(j, 0, w);
                 for (uint32_t p0 = 64 * kKG; p0 < steps; p0 += 64 * kKG) {  // runs longer than one pass (rare)
                     issue(j, p0, w);
