@@ -79,6 +79,8 @@ def parse_args(argv=None):
     p.add_argument("--cpu-baseline-sec", type=float, default=8.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-box-state", action="store_true", help="skip the sysfs record of clocks / partitions")
+    p.add_argument("--step-events", type=int, default=1, help=argparse.SUPPRESS)  # A/B: 0 = no per-step events
+    p.add_argument("--decode-events", type=int, default=1, help=argparse.SUPPRESS)  # A/B: 0 = decode not bracketed
     p.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--share-gpu", action="store_true",
                    help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
@@ -240,7 +242,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     # roofline kernel); the other kernels are timed in a separate pass below,
     # so the timed steps carry no event packets between the other launches
     q.timing_stages(["rx_decode"])
-    q.enable_timing(True)
+    q.enable_timing(bool(args.decode_events))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -249,7 +251,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     evs[0].record(stream)
     for i in range(args.steps):
         step()
-        evs[i + 1].record(stream)  # per-step GPU time for the median (no host sync inside)
+        if args.step_events or i + 1 == args.steps:
+            evs[i + 1].record(stream)  # per-step GPU time for the median (no host sync inside)
     # the histogram's slice pass runs once per few staged batches: the pending
     # one runs inside the timed region, so every timed batch is in the table
     q.flush_histogram()
@@ -280,13 +283,15 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     torch.cuda.synchronize(dev)
     q.enable_timing(False)
     for name, s in q.read_timing().items():
-        if name != "rx_decode":
+        if name != "rx_decode" or not args.decode_events:
             stages[name] = dict(s, batches=bd_steps)
-    stages["rx_decode"]["batches"] = args.steps
+    if args.decode_events:
+        stages["rx_decode"]["batches"] = args.steps
     hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass, at most
     slice_passes = stages.get("rx_slice_histo", {}).get("launches", 0)
 
-    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) if args.step_events else \
+        [evs[0].elapsed_time(evs[args.steps]) / args.steps]
     total_pkts = n * args.steps * world
     mpkts = total_pkts / elapsed / 1e6
     frame_gbs = frame_bytes * args.steps * world / elapsed / 1e9

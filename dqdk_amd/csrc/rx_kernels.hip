@@ -2492,7 +2492,6 @@ struct SliceLds {
     uint32_t b_i0[kSliceMaxSlots], b_end[kSliceMaxSlots];  // the bucket's first item / inclusive prefix of its items per staged batch
     uint32_t w_tot[kSliceThreads / 64];
     uint32_t total;
-    uint32_t junk[64];  // DQDK_SLICE_TOUCH: the touches' LDS-DMA destination (never read)
 };
 constexpr uint32_t kDrainCap = 0xffffu - 0xffu;  // events per group: bins hold <= 255 after a drain
 
@@ -2713,33 +2712,6 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
                 }
             }
         };
-#ifndef DQDK_SLICE_TOUCH
-#define DQDK_SLICE_TOUCH 0
-#endif
-        // (A/B) the wave's next group's runs touched into L2 while this
-        // group is counted: one LDS-DMA dword per 128-B line (16 lanes an
-        // item; the destination is a junk word per lane, never read).  Inline
-        // asm, so hipcc's vmcnt bookkeeping does not see them: the group's own
-        // loads are waited for (a counted s_waitcnt) before they are issued,
-        // and the next group's loads, issued after them, retire after them.
-        auto touch = [&](uint32_t jn) {
-            const uint32_t q = min((uint32_t)lane >> 4, (uint32_t)kNI - 1u);
-            const uint32_t jj = jn + q * kWavesS;
-            const bool v = jj < nit;
-            if (!__ballot(v))
-                return;
-            const uint32_t jc = v ? jj : jn;
-            const uint32_t r = sl.s_run[jc < nit ? jc : 0u];
-            const uint32_t b0 = (2u * (r & 0xffffu)) & ~127u, b1 = 2u * (r >> 16);  // the run's bytes
-            uint32_t li = ((uint32_t)lane & 15u) * 128u;
-            li = b0 + li < b1 ? li : 0u;
-            const uint8_t* src = (const uint8_t*)(a.part2 + (uint64_t)sl.s_k[jc < nit ? jc : 0u] * a.part2_stride +
-                                                  (uint64_t)sl.s_base[jc < nit ? jc : 0u] * kPartChunk) + b0 + li;
-            const uint32_t dst = rfl((uint32_t)(uintptr_t)sl.junk);
-            uint32_t keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-        };
         for (uint32_t gs = 0; gs < nit;) {
             if (drains) {  // the group: the longest run of entries whose events fit kDrainCap - since
                 const uint32_t base = gs ? rfl(sl.s_pin[gs - 1]) : 0u, lim = kDrainCap - since;
@@ -2757,10 +2729,6 @@ __device__ __forceinline__ void slice_histo(const HistoArgs& a, uint32_t s, uint
             for (uint32_t j = gs + (uint32_t)wave; j < ge; j += kGrp) {
                 uint32_t w[kNI][kKG];
                 const uint32_t steps = issue(j, 0, w);
-                if (DQDK_SLICE_TOUCH) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this group's loads, known to hipcc
-                    touch(j + kGrp);
-                }
                 count(j, 0, w);
                 for (uint32_t p0 = 64 * kKG; p0 < steps; p0 += 64 * kKG) {  // runs longer than one pass (rare)
                     issue(j, p0, w);
