@@ -79,8 +79,13 @@ def parse_args(argv=None):
     p.add_argument("--cpu-baseline-sec", type=float, default=8.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-box-state", action="store_true", help="skip the sysfs record of clocks / partitions")
-    p.add_argument("--step-events", type=int, default=1, help=argparse.SUPPRESS)  # A/B: 0 = no per-step events
-    p.add_argument("--decode-events", type=int, default=1, help=argparse.SUPPRESS)  # A/B: 0 = decode not bracketed
+    # events inside the timed region (r06h: a torch event per step cost ~4 us a
+    # step, HIP events around every decode ~6 us): the decode is bracketed on
+    # every --decode-event-every'th batch (its mean launch time, the roofline's
+    # denominator, over those launches), one torch event pair spans the region
+    p.add_argument("--step-events", type=int, default=0, help=argparse.SUPPRESS)  # 1: a torch event every step
+    p.add_argument("--decode-events", type=int, default=1, help=argparse.SUPPRESS)  # 0: decode timed in the breakdown
+    p.add_argument("--decode-event-every", type=int, default=4, help=argparse.SUPPRESS)
     p.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--share-gpu", action="store_true",
                    help="rehearsal on fewer GPUs than ranks: rank r uses GPU r %% count, control-plane "
@@ -239,10 +244,11 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     torch.cuda.synchronize(dev)
     q.read_timing()  # discard
     # only rx_decode is bracketed by HIP events inside the timed region (the
-    # roofline kernel); the other kernels are timed in a separate pass below,
-    # so the timed steps carry no event packets between the other launches
+    # roofline kernel), on every `every`-th batch (each event pair is GPU
+    # time in the step: r06h); the other kernels are timed in a separate pass
+    # below, so the timed steps carry no event packets between their launches
     q.timing_stages(["rx_decode"])
-    q.enable_timing(bool(args.decode_events))
+    every = max(args.decode_event_every, 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -250,6 +256,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i in range(args.steps):
+        q.enable_timing(bool(args.decode_events) and i % every == 0)  # (a host flag: no GPU work)
         step()
         if args.step_events or i + 1 == args.steps:
             evs[i + 1].record(stream)  # per-step GPU time for the median (no host sync inside)
@@ -286,7 +293,7 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
         if name != "rx_decode" or not args.decode_events:
             stages[name] = dict(s, batches=bd_steps)
     if args.decode_events:
-        stages["rx_decode"]["batches"] = args.steps
+        stages["rx_decode"]["batches"] = stages["rx_decode"]["launches"]  # the bracketed ones
     hist_k = q.histogram_batches_per_pass()  # partitioned batches per slice pass, at most
     slice_passes = stages.get("rx_slice_histo", {}).get("launches", 0)
 
@@ -393,6 +400,8 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
                 "frac": dec.get("frac_hbm"), "traffic": traffic,
                 "alg_bytes_per_frame": round(16 + Lm + 8 + (4 * E if keys_written else 0), 1),
                 "frames_per_launch": n,
+                # the decode launches bracketed by HIP events inside the timed region (of args.steps)
+                "timed_launches": dec.get("launches"), "timed_region_launches": args.steps,
                 "measured_stream_read_GB_s": round(stream_gbs, 1),
                 "frac_of_measured_stream": round(dec["GB_s"] / stream_gbs, 4) if dec else None,
                 "measured_frames_pattern_GB_s": pattern,

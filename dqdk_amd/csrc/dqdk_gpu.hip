@@ -1234,6 +1234,14 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
                     return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
             }
             q->hist_k = k;
+            // every slot's per-batch words zero from the start, so no batch
+            // of the first slice pass pays clean_slot's memsets (four fill
+            // launches per batch; a long capture's later passes find the
+            // slots re-zeroed by rx_part2 anyway)
+            if ((e = hipMemset(q->d_hscratch, 0, (size_t)k * q->scratch_words * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipStreamSynchronize(nullptr)) != hipSuccess)
+                return cleanup(fail("hipMemset(slot scratch)", e));
+            q->slot_dirty.assign(k, 0);
         }
     }
     *out = q;
