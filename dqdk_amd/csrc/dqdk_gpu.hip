@@ -71,9 +71,10 @@ struct DevGuard {
         return fail("hipSetDevice", dev_guard_.e)
 
 constexpr int kStages = DQDK_GPU_TIMING_STAGES;
-// (rx_fixup: on the fused path, the launch of rx_part1_kernel that takes the
-// decode's piece scans, checksum-failed frames and overflow list; stage 5 is
-// unused since rx_part2 derives its items itself)
+// (rx_fixup: on the fused path, the launch of rx_part1_kernel that groups a
+// long overflow list for rx_part2 -- since round 6 only after a batch whose
+// list passed kOvfAtomicMax; stage 5 is unused since rx_part2 derives its
+// items itself)
 enum Stage { kStDecode, kStAbort, kStCount, kStAtomic, kStPart1, kStPrep, kStPart2, kStSlice, kStUnused8, kStFixup };  // 5, 8: retired kernels
 const char* const kStageNames[kStages] = {"rx_decode", "rx_abort", "rx_count",       "rx_histo_atomic",
                                           "rx_part1",  "(unused)", "rx_part2",       "rx_slice_histo",
@@ -199,7 +200,6 @@ struct dqdk_gpu_queue {
     // known to be zero: set until a batch's rx_part2 (which re-zeroes them
     // at its end) is enqueued on the slot, memset on the next use otherwise
     std::vector<uint8_t> slot_dirty;
-    uint32_t* d_fix = nullptr;     // fused path: decoded frames that failed afterwards (max_batch)
     uint32_t* d_ovf_blk = nullptr; // fused path: per-block overflow regions (in d_part1's rx_part1 region)
     uint64_t ovf_blk_elems = 0;    // grid * ovf_cap_blk
     uint64_t fused_elems = 0;      // fused path: pieces region (0: the fused path is off)
@@ -215,6 +215,7 @@ struct dqdk_gpu_queue {
     bool p2zero_off = false;       // DQDK_GPU_P2ZERO=0: memset the slot's counters before every batch
     bool small_off = false;        // DQDK_GPU_SMALL=0: small batches take the three-launch form too
     uint32_t tile_frames = 0;      // DQDK_GPU_TILE_FRAMES: records-path decode frames per wave tile (0: 64)
+    int ovf_list_mode = -1;        // DQDK_GPU_OVF_LIST: fused overflow keys 0 = atomics, 1 = listed + grouped (-1: by the last batch)
     // Staging placement probe: the fused decode's rate
     // depends on where its piece buffer (d_part1, the decode's write stream)
     // lands physically relative to the image it reads -- 2.12 vs 2.35 ms at
@@ -271,6 +272,8 @@ struct dqdk_gpu_queue {
     dqdk_gpu_desc_t* h_desc = nullptr;
     dqdk_gpu_rx_result_t* h_res = nullptr;
     uint64_t* h_batch = nullptr;
+    uint64_t* h_ovf = nullptr;      // fused path: the last batch's overflow keys (host-mapped, rx_part2 writes)
+    uint64_t* h_ovf_dev = nullptr;
     const dqdk_gpu_desc_t* h_desc_dev = nullptr;
     dqdk_gpu_rx_result_t* h_res_dev = nullptr;
     uint64_t* h_batch_dev = nullptr;
@@ -506,14 +509,18 @@ int launch_histo(dqdk_gpu_queue* q, uint32_t n, const dqdk_gpu_rx_result_t* d_re
                                                (uint32_t)q->cu_count * (uint32_t)kP1BlocksPerCu);
     const uint32_t grid_l2 = std::min<uint32_t>(chunks + (uint32_t)(kL1Buckets * kSegsPerBucket),
                                                 (uint32_t)q->cu_count * (uint32_t)kP2BlocksPerCu);
-    {
-        // fused: the decode's piece scans and checksum-failed frames,
-        // then the overflow list (usually empty), timed as "rx_fixup"
+    // fused path: the decode takes back checksum-failed frames itself and, in
+    // its usual form, adds its overflow keys to the table by device atomics
+    // (round 6: one launch less per batch); after a batch with more than
+    // kOvfAtomicMax overflow keys (rx_part2 reports the count into
+    // host-mapped memory) the next batches list them instead (RxArgs::ovf_list)
+    // and rx_part1 groups the list for rx_part2, timed as "rx_fixup"
+    if (fused)
+        ha.ovf_out = q->h_ovf_dev;
+    if (!fused || ra.ovf_list) {
         StageTimer t(q, fused ? kStFixup : kStPart1);
-        hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ra, ha);
+        hipLaunchKernelGGL(rx_part1_kernel, dim3(grid_p), dim3(kP1Threads), 0, q->stream, ha);
     }
-    if (q->publish && fused)  // rx_fixup was the last reader of the caller's frames
-        HIPCHK(hipEventRecord(q->ev_read, q->stream));
     ha.p2_ticket = (uint32_t*)(q->d_batch + kPart2TicketWord);
     {
         StageTimer t(q, kStPart2);
@@ -678,6 +685,8 @@ int read_knobs(dqdk_gpu_queue* q)
     q->fmap = env("DQDK_GPU_FRAME_MAP") ? (uint32_t)(atoi(env("DQDK_GPU_FRAME_MAP")) != 0) : 0u;
     q->p2zero_off = env("DQDK_GPU_P2ZERO") && !strcmp(env("DQDK_GPU_P2ZERO"), "0");
     q->small_off = env("DQDK_GPU_SMALL") && !strcmp(env("DQDK_GPU_SMALL"), "0");
+    if (const char* v = env("DQDK_GPU_OVF_LIST"))
+        q->ovf_list_mode = atoi(v) != 0 ? 1 : 0;
     if (const char* v = env("DQDK_GPU_TILE_FRAMES"))  // records-path decode: frames per wave tile (1-64)
         q->tile_frames = std::min<uint32_t>(64, std::max<uint32_t>(1, (uint32_t)atoi(v)));
     q->probe = env("DQDK_GPU_STAGING_PROBE") && !strcmp(env("DQDK_GPU_STAGING_PROBE"), "0") ? 0 : 1;
@@ -707,7 +716,7 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
     // accounting (the frames after the first failure are known only after
     // the decode; the records path counts exactly the accounted frames).
     const FusedGeom fg = fused_geom(n, q->E, (uint64_t)q->dec_cus);
-    const bool fused = partitioned && !d_keys && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT) && q->d_fix &&
+    const bool fused = partitioned && !d_keys && !(q->cfg.flags & DQDK_GPU_F_BATCH_ABORT) && q->d_ovf &&
                        !(q->cfg.flags & DQDK_GPU_F_HISTO_UNFUSED) &&
                        (uint64_t)kL1Buckets * fg.region <= q->fused_elems;
     if (!fused && q->histo && q->E) {
@@ -747,7 +756,10 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         ra.piece_words = fg.words;
         ra.region = fg.region;
         ra.ovf = q->d_ovf;
-        ra.fix = q->d_fix;
+        // overflow keys listed for rx_part1's grouping only after a batch
+        // that overflowed a lot (a heuristic: either form counts every key once)
+        ra.ovf_list = q->ovf_list_mode >= 0 ? (uint32_t)q->ovf_list_mode
+                      : q->h_ovf && __atomic_load_n(q->h_ovf, __ATOMIC_RELAXED) > kOvfAtomicMax ? 1u : 0u;
         ra.round_windows = q->round_windows;
         const uint32_t grid = fg.grid;
         // private overflow regions of ovf_cap_blk keys (past them: the table)
@@ -817,10 +829,9 @@ int launch_batch(dqdk_gpu_queue* q, const uint8_t* d_umem, uint64_t umem_size, c
         }
         HIPCHK(hipGetLastError());
     }
-    // the records path reads no caller memory past this point (the fused
-    // path's rx_fixup re-reads the frames of checksum-failed ones: its mark
-    // is in launch_histo)
-    if (q->publish && !fused)
+    // no kernel reads caller memory past this point (since round 6 the fused
+    // decode takes back its checksum-failed frames itself)
+    if (q->publish)
         HIPCHK(hipEventRecord(q->ev_read, q->stream));
 
     if (q->histo && q->E)
@@ -1153,6 +1164,15 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
         (e = hipMemset(q->d_batch, 0, kBatchScratch * sizeof(uint64_t))) != hipSuccess)
         return cleanup(fail("hipMemset", e));
     if (q->histo) {
+        // the fused path's overflow-list length, written by rx_part2 into host
+        // memory the host reads without a sync (launch_histo's grouping choice)
+        if ((e = hipHostMalloc(&q->h_ovf, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+                hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&q->h_ovf_dev, q->h_ovf, 0)) != hipSuccess)
+            return cleanup(fail("hipHostMalloc(overflow length)", e));
+        *q->h_ovf = 0;
+    }
+    if (q->histo) {
         if ((e = dev_alloc(&q->d_hist, DQDK_TRISTAN_HISTO_ENTRIES * sizeof(uint32_t), q->alloc_kind)) != hipSuccess ||
             (e = dev_alloc(&q->d_lo, DQDK_TRISTAN_HISTO_ENTRIES, q->alloc_kind)) != hipSuccess)
             return cleanup((fail("hipMalloc(histogram)", e), -ENOMEM));
@@ -1192,8 +1212,7 @@ int dqdk_gpu_queue_create(int device, const dqdk_gpu_cfg_t* cfg, uint32_t max_ba
             if (q->fused_elems) {
                 q->part1_elems = q->piece_shift + q->fused_elems + q->ovf_blk_elems + kStagePad;
                 if ((e = dev_alloc(&q->d_part1, q->part1_elems * 4, q->alloc_kind)) != hipSuccess ||
-                    (e = hipMalloc(&q->d_ovf, q->ovf_blk_elems * sizeof(uint32_t))) != hipSuccess ||
-                    (e = hipMalloc(&q->d_fix, (size_t)max_batch * sizeof(uint32_t))) != hipSuccess)
+                    (e = hipMalloc(&q->d_ovf, q->ovf_blk_elems * sizeof(uint32_t))) != hipSuccess)
                     return cleanup((fail("hipMalloc(histogram staging)", e), -ENOMEM));
                 // (the overflow regions sit past every shifted piece region; rx_part1's
                 // output, written once they are dead, may overlap them)
@@ -1358,7 +1377,6 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     dfree(q->d_part2, "hipFree(part2 staging)");
     dfree(q->d_runs, "hipFree(part2 runs)");
     dfree(q->d_hscratch, "hipFree(slot scratch)");
-    dfree(q->d_fix, "hipFree(fixup list)");
     dfree(q->d_desc, "hipFree(descriptors)");
     dfree(q->d_res, "hipFree(results)");
     dfree(q->d_raw_blk, "hipFree(raw offsets)");
@@ -1372,6 +1390,7 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     hfree(q->h_desc, "hipHostFree(pinned descriptors)");
     hfree(q->h_res, "hipHostFree(pinned results)");
     hfree(q->h_batch, "hipHostFree(pinned counters)");
+    hfree(q->h_ovf, "hipHostFree(overflow length)");
     if (q->ev_read)
         chk(hipEventDestroy(q->ev_read), "hipEventDestroy(ev_read)");
     if (q->raw_stream)

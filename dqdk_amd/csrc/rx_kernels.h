@@ -96,18 +96,23 @@ constexpr int kOffCnt1 = 0;         // [kL1Buckets + 1] keys per bucket: decode 
                                     //   overflow keys per bucket (fused path)                 -- zeroed per batch
 constexpr int kOffCur1 = 288;       // [kL1Buckets] keys written per bucket by rx_part1         -- zeroed per batch
 constexpr int kOffOvfN = 577;       // fused path: keys sent to the overflow list               -- zeroed per batch
-constexpr int kOffFixN = 578;       // fused path: decoded frames whose final status is not OK  -- zeroed per batch
-constexpr int kZeroWords = 584;
+constexpr int kOffFixN = 578;       // (retired in round 6: the fused decode takes back failed frames itself)
+// fused path: each bucket's key triples over all its pieces (the decode's
+// blocks add their pieces' by device atomics: rx_part2's segment sizes), one
+// 128-B line per bucket: 256 blocks adding to words of a few shared lines
+// serialise at the memory side (r06i: decode +12 %)               -- zeroed per batch
+constexpr int kTotStride = 32;
+constexpr int kOffPieceTotT = 608;  // [kL1Buckets] at stride kTotStride words
+constexpr int kZeroWords = kOffPieceTotT + kL1Buckets * kTotStride;
 constexpr int kMaxFusedGrid = 256;  // fused decode blocks (one per CU)
 constexpr int kOffOff1 = kZeroWords;  // [kL1Buckets + 1] bucket starts of rx_part1's output (prep)
 constexpr int kOffIstart = kOffOff1 + 288;  // [kL1Buckets + 1] first part2 item of each bucket; [284] = items (rx_part2)
-// fused path: keys of each (bucket, block) piece [kL1Buckets][kMaxFusedGrid] (decode),
-// and per bucket the exclusive scans of its pieces' keys and of their key
-// triples [kL1Buckets][kMaxFusedGrid + 1] each (rx_part1's prologue)
+// fused path: keys of each (bucket, block) piece [kL1Buckets][kMaxFusedGrid]
+// (decode; rx_part2 scans a bucket's row into its pieces' starts per item)
 constexpr int kOffPieceN = kOffIstart + 288;
-constexpr int kOffPiecePre = kOffPieceN + kL1Buckets * kMaxFusedGrid;
-constexpr int kOffPiecePreT = kOffPiecePre + kL1Buckets * (kMaxFusedGrid + 1);
-constexpr int kOffEnd = kOffPiecePreT + kL1Buckets * (kMaxFusedGrid + 1);
+constexpr int kOffEnd = kOffPieceN + kL1Buckets * kMaxFusedGrid;
+static_assert(kOffFixN < kOffPieceTotT && kOffPieceTotT % kTotStride == 0 && kZeroWords % 16 == 0, "scratch layout");
+static_assert(kOffPieceN % 4 == 0 && kMaxFusedGrid % 4 == 0, "rx_part2 loads a bucket's piece sizes 16 B at a time");
 constexpr int kSegsPerBucket = 2;  // fused: the bucket's pieces (one gathered sequence), then rx_part1's overflow run
 // items of a batch of nk keys: one per started chunk of each segment (a
 // bucket's gathered triples number at most its keys / 3 + one per piece)
@@ -185,7 +190,8 @@ struct RxArgs {
     uint32_t* ovf_blk;        // per-block private overflow regions (gridDim.x * ovf_blk_cap keys)
     uint32_t ovf_blk_cap;     // keys per region; past it (pathological spectra) a key is added to
     uint32_t* hist;           //   the table's base plane by a device atomic (exact: value = base + low)
-    uint32_t* fix;            // decoded frames whose final status is not OK (n)
+    uint32_t ovf_list;        // overflow keys: 0 = to the table by device atomics at the block's end;
+                              //   1 = to the overflow list (kOffCnt1 per bucket) for rx_part1's grouping
     uint32_t round_windows;   // windows per wave per round (multiple of the ring depth)
     uint32_t tile_frames;     // records path: frames per wave tile (0 = 64; fewer spread a small
                               //   batch over more waves, the host drop-in's zero-copy frames)
@@ -249,6 +255,10 @@ struct HistoArgs {
     // scratch [0, kZeroWords), the per-batch counters, once every block has
     // read them: the slot is clean for its next batch without a memset
     uint32_t* p2_ticket;
+    // fused path: the last block reports the batch's overflow keys
+    // (scratch[kOffOvfN]) to ovf_out, host-mapped: the host's choice of the
+    // next batches' overflow form (RxArgs::ovf_list)
+    uint64_t* ovf_out;
 };
 
 // Frame-processor plugin (dqdk_gpu_frame_processor, frame_processor.hip):
@@ -276,7 +286,7 @@ __global__ void rx_abort_kernel(CountArgs a);
 __global__ void rx_small_kernel(RxArgs ra, CountArgs ca);  // gridDim 1, n <= kTile, records path
 __global__ void rx_count_kernel(CountArgs a);
 __global__ void rx_histo_atomic_kernel(HistoArgs a);
-__global__ void rx_part1_kernel(RxArgs ra, HistoArgs a);
+__global__ void rx_part1_kernel(HistoArgs a);
 template <int kLdAux>
 __global__ void rx_part2_kernel(HistoArgs a);
 __global__ void rx_slice_histo_kernel(HistoArgs a);

@@ -1113,6 +1113,34 @@ struct FusedLds {
     alignas(8) uint32_t fc[kFoldWords];  // folded counters of the block (FoldWord; the bytes word pair is a u64)
 };
 
+// A frame the fused decode staged but whose final status is not OK (it
+// failed the UDP checksum): its events are subtracted from the table's base
+// plane (u32 wrap: +1 later, -1 now, leaves every bin exact), the wave's
+// lanes taking its events in turn.  Event bytes are read as the decode read
+// them (zeros at or past umem_size).  (Before round 6 the frame was listed
+// and rx_part1 took it back, a launch per batch.)
+__device__ __forceinline__ void takeback_frame(const RxArgs& a, uint32_t i, uint32_t lane)
+{
+    const uint64_t addr = a.desc[i].addr;
+    const uint64_t ihl_at = addr + 14;
+    const uint32_t ihl = ihl_at < a.umem_size ? (a.umem[ihl_at] & 0xfu) : 0u;
+    const uint64_t p = addr + 14 + 4 * ihl + 8;  // get_udp_payload's payload (dqdk.c:205-206)
+    for (uint32_t e = lane; e < a.E; e += 64) {
+        uint8_t ev[10];
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+            const uint64_t o = p + 16ull * e + (uint64_t)j;
+            ev[j] = o < a.umem_size ? a.umem[o] : (uint8_t)0;
+        }
+        const uint32_t ch = ev[2] | ((uint32_t)ev[3] << 8);
+        const uint32_t hc = ev[8] & 7u;
+        const uint32_t bin = ev[5] | ((uint32_t)ev[6] << 8);
+        if (ch < kChannels && hc < kHists)
+            __hip_atomic_fetch_sub(&a.hist[(ch * kHists + hc) * DQDK_TRISTAN_BINS + bin], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Block barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release + acquire: on gfx950 that is s_waitcnt vmcnt(0) before s_barrier,
 // which would wait for every ring load in flight and every run store of the
@@ -1199,6 +1227,9 @@ __device__ __forceinline__ void fused_pair(const RxArgs& a, const u32x4& va, con
 
 #ifndef DQDK_CEIL
 #define DQDK_CEIL 0
+#endif
+#ifndef DQDK_NO_TOT  // (A/B timing only: the segment sizes not published; tables wrong)
+#define DQDK_NO_TOT 0
 #endif
 #if DQDK_CEIL
 // Timing-only CEILING of the fused decode's read + write pattern (VERDICT r5
@@ -1613,25 +1644,42 @@ __global__ void __launch_bounds__(kFThreads, 1) rx_decode_fused_kernel(RxArgs a)
         phase_c(a, i, live, stream, fi, r, sum_t, sum_oob, u32x4{0u, 0u, 0u, 0u});
         if (a.fold)
             fold_frames(a, lds.fc, live, r, i, lane);
-        // decoded, then failed the UDP checksum: its keys are staged already (rx_fixup takes them back)
-        if (live && (fi.work & 1) && r.status != DQDK_RX_OK)
-            a.fix[atomicAdd(&a.scratch[kOffFixN], 1u)] = i;
+        // decoded, then failed the UDP checksum: its keys are staged already,
+        // so the wave takes their events back from the table now (rare)
+        for (uint64_t fm = __ballot(live && (fi.work & 1) && r.status != DQDK_RX_OK); fm; fm &= fm - 1)
+            takeback_frame(a, rdl(i, (uint32_t)__builtin_ctzll(fm)), (uint32_t)lane);
     }
     // the keys still staged, then the piece sizes for rx_part1 / rx_part2
     lds_barrier();
     if (!DQDK_CEIL)
         fused_flush<kLines, true>(a, lds, lane, wave, fcur, ovf_rsrc);
     {
+        // this block's piece sizes, and (device atomics, executed at the
+        // memory side: no fence) their triples per bucket, rx_part2's segment sizes
         const uint32_t b = wave + (uint32_t)kFWaves * (uint32_t)lane;
-        if (b < (uint32_t)kL1Buckets)
+        if (b < (uint32_t)kL1Buckets) {
             a.scratch[kOffPieceN + b * kMaxFusedGrid + blockIdx.x] = fcur;
+            if (fcur && !DQDK_NO_TOT)
+                __hip_atomic_fetch_add(&a.scratch[kOffPieceTotT + b * kTotStride], (fcur + 2u) / 3u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     // the block's private overflow region is appended to the overflow list
     __syncthreads();  // (also orders the region's stores before the copy below)
     // (the last flush left every stage count at 0: they count the region's
     // keys per bucket here, then one device atomic per bucket per block)
     const uint32_t nov = min(lds.ovf_n, a.ovf_blk_cap);  // (the keys past the region went to the table)
-    if (nov) {
+    if (nov && !a.ovf_list) {
+        // each key to the table's base plane by a relaxed device atomic (the
+        // reference's ++ at src/tristan.c:243); the count, for the host's
+        // choice of the next batches' form (rx_part2 reports it)
+        if (tid == 0)
+            atomicAdd(&a.scratch[kOffOvfN], nov);
+        for (uint32_t t = (uint32_t)tid; t < nov; t += kFThreads)
+            __hip_atomic_fetch_add(&a.hist[ovf_blk[t]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (nov) {
+        // the list form (after a batch with a long list): rx_part1 groups it
+        // by bucket for rx_part2
         if (tid == 0)
             lds.wtot[0] = atomicAdd(&a.scratch[kOffOvfN], nov);
         __syncthreads();
@@ -1661,70 +1709,6 @@ template __global__ void rx_decode_fused_kernel<0, true, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, false, true>(RxArgs);
 template __global__ void rx_decode_fused_kernel<2, true, true>(RxArgs);
 #endif
-
-// Frames the fused decode staged but whose final status is not OK: subtract
-// their events from the table (u32 wrap: +1 then -1 leaves every bin exact).
-// Event bytes are read as the decode read them (zeros at or past umem_size).
-// Runs as rx_part1's prologue on the fused path (a launch of its own cost
-// more than its work); gw / nw: the calling wave's index / the grid's waves.
-__device__ __forceinline__ void fused_fixup(const RxArgs& a, const HistoArgs& h, uint32_t gw, uint32_t nw)
-{
-    const uint32_t nfix = a.scratch[kOffFixN];
-    const int lane = threadIdx.x & 63;
-    // first, one wave per bucket: the exclusive scans of its pieces' keys and
-    // key triples (rx_part2's segment sizes, piece starts and valid keys)
-    for (uint32_t b = gw; b < (uint32_t)kL1Buckets; b += nw) {
-        const uint32_t* cn = a.scratch + kOffPieceN + b * kMaxFusedGrid;
-        uint32_t* pre = a.scratch + kOffPiecePre + b * (kMaxFusedGrid + 1);
-        uint32_t* preT = a.scratch + kOffPiecePreT + b * (kMaxFusedGrid + 1);
-        uint32_t v[4], vt[4], sum = 0, sumt = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t blk = (uint32_t)lane * 4u + i;
-            v[i] = blk < h.fgrid ? cn[blk] : 0u;
-            vt[i] = (v[i] + 2u) / 3u;
-            sum += v[i];
-            sumt += vt[i];
-        }
-        const uint32_t incl = wave_incl_scan_dpp(sum), inclt = wave_incl_scan_dpp(sumt);
-        uint32_t run = incl - sum, runt = inclt - sumt;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t blk = (uint32_t)lane * 4u + i;
-            if (blk < h.fgrid) {
-                pre[blk] = run;
-                preT[blk] = runt;
-            }
-            run += v[i];
-            runt += vt[i];
-        }
-        if (lane == 63) {
-            pre[h.fgrid] = incl;
-            preT[h.fgrid] = inclt;
-        }
-    }
-    for (uint32_t k = gw; k < nfix; k += nw) {
-        const uint32_t i = a.fix[k];
-        const uint64_t addr = a.desc[i].addr;
-        const uint64_t ihl_at = addr + 14;
-        const uint32_t ihl = ihl_at < a.umem_size ? (a.umem[ihl_at] & 0xfu) : 0u;
-        const uint64_t p = addr + 14 + 4 * ihl + 8;  // get_udp_payload's payload (dqdk.c:205-206)
-        for (uint32_t e = (uint32_t)lane; e < a.E; e += 64) {
-            uint8_t ev[10];
-#pragma unroll
-            for (int j = 0; j < 10; j++) {
-                const uint64_t o = p + 16ull * e + (uint64_t)j;
-                ev[j] = o < a.umem_size ? a.umem[o] : (uint8_t)0;
-            }
-            const uint32_t ch = ev[2] | ((uint32_t)ev[3] << 8);
-            const uint32_t hc = ev[8] & 7u;
-            const uint32_t bin = ev[5] | ((uint32_t)ev[6] << 8);
-            if (ch < kChannels && hc < kHists)
-                __hip_atomic_fetch_sub(&h.hist[(ch * kHists + hc) * DQDK_TRISTAN_BINS + bin], 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Counters (fetch_xsk accounting, src/dqdk.c:252-322; tristan.c:327-328).
@@ -1977,10 +1961,8 @@ constexpr bool kP1Pipe = DQDK_P1_PIPE;  // part1 loads chunk c+1 while chunk c i
 // after the scatter.  One 32K-key chunk per block (128 KB of LDS, one block
 // per CU) halves the reservations per key of a 16K chunk and doubles the
 // average run written per bucket.
-__global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(RxArgs ra, HistoArgs a)
+__global__ void __launch_bounds__(kP1Threads, kP1MinWaves) rx_part1_kernel(HistoArgs a)
 {
-    if (a.fused)  // the fused decode's piece scans and checksum-failed frames
-        fused_fixup(ra, a, (blockIdx.x * kP1Threads + threadIdx.x) >> 6, (gridDim.x * kP1Threads) >> 6);
     __shared__ uint32_t stage[kP1Chunk];
     __shared__ uint32_t off1[kL1Buckets + 1];
     __shared__ uint32_t lcnt[kL1Buckets];
@@ -2132,7 +2114,7 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             c = a.scratch[kOffCur1 + b];
             per = kPartChunk;
         } else {                    // the bucket's pieces: key triples
-            c = a.scratch[kOffPiecePreT + b * (kMaxFusedGrid + 1) + a.fgrid];
+            c = a.scratch[kOffPieceTotT + b * kTotStride];  // (the decode's blocks summed their pieces' triples)
             per = kPartTriples;
         }
         s_cnt[tid] = c;
@@ -2182,30 +2164,50 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
         g.base8 = g.gath ? 0u : (uint32_t)((a.part1_base + rfl(off1[g.b])) / kBucketAlign) + g.s0 / kBucketAlign;
         return g;
     };
-    // a gathered item: its bucket's piece starts (then a barrier)
-    auto stage_pieces = [&](const Item& g, int pb) {
-        if (g.gath && (uint32_t)tid <= a.fgrid) {
-            const uint32_t t = opaque((uint32_t)tid);
-            prt[pb][t] = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + t];
-            prk[pb][t] = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + t];
-        }
-    };
-    // the same in two halves: the loads early (into registers), the LDS
-    // stores late, so their latency passes under the work between
-    uint32_t pst = 0, psk = 0;
+    // a gathered item: its bucket's piece starts, the exclusive scans of the
+    // decode blocks' piece sizes in keys (prk) and key triples (prt), by wave
+    // 0 (four pieces a lane, DPP scans) from the sizes the decode wrote --
+    // in two halves: the sizes' load early (into registers), the scans and
+    // LDS stores late, so the load's latency passes under the work between
+    // (then a barrier before they are read)
+    u32x4_t pcn = u32x4_t{0u, 0u, 0u, 0u};
     auto fetch_pieces = [&](const Item& g) {
-        if (g.gath && (uint32_t)tid <= a.fgrid) {
-            const uint32_t t = opaque((uint32_t)tid);
-            pst = a.scratch[kOffPiecePreT + g.b * (kMaxFusedGrid + 1) + t];
-            psk = a.scratch[kOffPiecePre + g.b * (kMaxFusedGrid + 1) + t];
+        if (g.gath && wave == 0) {
+            const uint32_t l = opaque(lane);
+            pcn = *(const u32x4_t*)(a.scratch + kOffPieceN + g.b * kMaxFusedGrid + 4u * l);
         }
     };
     auto put_pieces = [&](const Item& g, int pb) {
-        if (g.gath && (uint32_t)tid <= a.fgrid) {
-            const uint32_t t = opaque((uint32_t)tid);
-            prt[pb][t] = pst;
-            prk[pb][t] = psk;
+        if (g.gath && wave == 0) {
+            const uint32_t l = opaque(lane);
+            uint32_t v[4] = {pcn.x, pcn.y, pcn.z, pcn.w}, sum = 0, sumt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                v[i] = 4u * l + (uint32_t)i < a.fgrid ? v[i] : 0u;  // (rows past the grid: stale)
+                sum += v[i];
+                sumt += (v[i] + 2u) / 3u;
+            }
+            const uint32_t incl = wave_incl_scan_dpp(sum), inclt = wave_incl_scan_dpp(sumt);
+            uint32_t run = incl - sum, runt = inclt - sumt;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t blk = 4u * l + (uint32_t)i;
+                if (blk < a.fgrid) {
+                    prk[pb][blk] = run;
+                    prt[pb][blk] = runt;
+                }
+                run += v[i];
+                runt += (v[i] + 2u) / 3u;
+            }
+            if (l == 63) {
+                prk[pb][a.fgrid] = incl;
+                prt[pb][a.fgrid] = inclt;
+            }
         }
+    };
+    auto stage_pieces = [&](const Item& g, int pb) {
+        fetch_pieces(g);
+        put_pieces(g, pb);
     };
     // slots: gathered items, wave w takes the item's triples [384w, 384w +
     // 384), 64 per load (load j: triple 384w + 64j + lane -> keys 3j .. 3j + 2
@@ -2457,6 +2459,9 @@ __global__ void __launch_bounds__(kPartThreads, DQDK_P2_WAVES) rx_part2_kernel(H
             p2_last = atomicAdd(a.p2_ticket, 1u) == gridDim.x - 1;
         __syncthreads();
         if (p2_last) {
+            if (fused && a.ovf_out && tid == 0)  // the batch's overflow, for the host's list-or-atomics choice
+                __hip_atomic_store(a.ovf_out, (uint64_t)a.scratch[kOffOvfN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __syncthreads();  // (read before it is zeroed)
             for (int w = tid; w < kZeroWords; w += kPartThreads)
                 a.scratch[w] = 0u;
             if (tid == 0)

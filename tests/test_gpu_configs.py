@@ -66,7 +66,9 @@ def test_configs3_four_queues_mixed_sizes_merged(records):
                              d_keys.data_ptr() if records else None)
             torch.cuda.synchronize()
             launched = {k for k, v in q.read_timing().items() if v["launches"]}
-            assert ("rx_fixup" in launched) == (not records), launched
+            # fused (no records): no rx_part1 (the decode takes back failed frames and adds its
+            # overflow keys itself, or lists them for rx_fixup's grouping); records: rx_part1
+            assert ("rx_part1" in launched) == records and "rx_part2" in launched, launched
             gres.append(d_res.cpu().numpy().view(D.RESULT_DTYPE))
             gcnt.append(q.counters())
             ores, ocnt, _ = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, want_keys=False, hist=otable,

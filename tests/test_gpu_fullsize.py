@@ -2,8 +2,8 @@
 
 bench.py runs histogram batches with NO record buffer: partitioned batches
 then take rx_decode_fused (keys bucketed in the decode's LDS stages and
-appended to per-block pieces, rx_fixup taking back frames that fail the UDP
-checksum afterwards, rx_part2 gathering the pieces), at 1M x 1500 B and
+appended to per-block pieces, the decode taking back frames that fail the
+UDP checksum afterwards, rx_part2 gathering the pieces), at 1M x 1500 B and
 1M x 9000 B (BASELINE north star) and 256K x 9000 B (configs[2]).  Here the
 same calls run on the same synthetic UMEM and every per-frame result, every
 counter and the WHOLE 2.38 GB table are compared with the oracle
@@ -12,9 +12,9 @@ counter and the WHOLE 2.38 GB table are compared with the oracle
 At 1M frames each of the 256 persistent decode blocks iterates four
 super-tiles (rx_kernels.hip, rx_decode_fused_kernel's `st` loop), so the
 piece cursors accumulate across super-tiles; the faulty variants give
-rx_fixup thousands of checksum-failed frames; the peaked variant fills
-the LDS stages and the per-block pieces of three buckets, so keys take the
-overflow path into rx_part1.
+the decode's take-back thousands of checksum-failed frames; the peaked
+variant fills the LDS stages and the per-block pieces of three buckets, so
+keys take the overflow path (device atomics, or the list rx_fixup groups).
 """
 import numpy as np
 import pytest
@@ -55,6 +55,14 @@ def run_bench_form(umem: np.ndarray, desc: np.ndarray, cfg: D.RxConfig, batches:
     return res, cnt, table, launches
 
 
+def fused_ran(launches: dict, batches: int) -> bool:
+    """The fused decode ran every batch: rx_part2 once a batch and no
+    rx_part1 (the records path's bucket grouping); rx_fixup, the fused path's
+    overflow grouping, only in the listed-overflow form."""
+    return launches.get("rx_part2", 0) == batches and launches.get("rx_part1", 0) == 0 and \
+        launches.get("rx_decode", 0) == batches
+
+
 def oracle_full(umem, desc, cfg):
     table = np.zeros(D.HISTO_ENTRIES, np.uint32)
     ores, ocnt, _ = O.rx_batch(umem, desc, cfg.payloadsz, cfg.mode, cfg.flags, want_keys=False, hist=table,
@@ -91,28 +99,34 @@ def test_fused_full_size_vs_oracle(n, L, stride, payloadsz, faulty):
     umem, desc = D.synth_umem(n, L, stride, faulty=faulty, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=payloadsz, flags=D.F_CSUM)  # bench.py's flags: auto histogram path
     res, cnt, table, launches = run_bench_form(umem, desc, cfg)
-    assert launches.get("rx_fixup", 0) == 1, launches  # the fused decode ran (rx_fixup is fused-only)
+    assert fused_ran(launches, 1), launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     assert_same(res, cnt, table, ores, ocnt, otable)
     if faulty:
-        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 1000  # rx_part1's fixup takes these back
+        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 1000  # the decode takes these back
         assert ocnt["oob_events"] > 0
     else:
         assert (ores["status"] == D.RX_OK).all()
 
 
-def test_fused_peaked_faulty_overflows_pieces():
+@pytest.mark.parametrize("ovf", ["auto", "atomics", "list"])
+def test_fused_peaked_faulty_overflows_pieces(monkeypatch, ovf):
     """1M x 1500 B, faulty headers and checksums AND a peaked spectrum (3/8
     of the events on four hot bins in three L1 buckets): the LDS stages of
     those buckets overflow every round and their per-block pieces fill, so
-    keys go through the block overflow regions into rx_part1; bins receive
-    far more than 65535 events.  Two batches:
-    the second adds onto the first in the table."""
+    keys go through the block overflow regions -- to the table by device
+    atomics, or listed and grouped by rx_part1 (DQDK_GPU_OVF_LIST; auto: by
+    the previous batch's overflow); bins receive far more than 65535 events.
+    Two batches: the second adds onto the first in the table."""
+    if ovf != "auto":
+        monkeypatch.setenv("DQDK_GPU_OVF_LIST", "1" if ovf == "list" else "0")
     n = 1 << 20
     umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, peaked=True, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
     res, cnt, table, launches = run_bench_form(umem, desc, cfg, batches=2)
-    assert launches.get("rx_fixup", 0) == 2 and launches.get("rx_slice_histo", 0) >= 1, launches
+    assert fused_ran(launches, 2) and launches.get("rx_slice_histo", 0) >= 1, launches
+    if ovf != "auto":
+        assert launches.get("rx_fixup", 0) == (2 if ovf == "list" else 0), launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     otable *= 2
     ocnt = {k: (v if k == "first_abort_idx" else 2 * v) for k, v in ocnt.items()}
@@ -120,19 +134,21 @@ def test_fused_peaked_faulty_overflows_pieces():
     assert int(otable.max()) > 0xFFFF
 
 
+@pytest.mark.parametrize("ovf", ["atomics", "list"])
 @pytest.mark.parametrize("L,stride,payloadsz", [(1500, 4096, 1458), (9000, 9216, 8958)])
-def test_fused_overflow_regions_spill_to_the_table(monkeypatch, L, stride, payloadsz):
+def test_fused_overflow_regions_spill_to_the_table(monkeypatch, L, stride, payloadsz, ovf):
     """The fused decode's per-block overflow regions are bounded (64K keys, or
     an eighth of a block's keys); past that a key goes to the table by a
     device atomic.  With the regions forced down to 64 keys (DQDK_GPU_OVF_BLK)
     and the peaked spectrum overflowing every round, most overflow keys take
     that spill: the table, results and counters still equal the oracle's."""
     monkeypatch.setenv("DQDK_GPU_OVF_BLK", "64")
+    monkeypatch.setenv("DQDK_GPU_OVF_LIST", "1" if ovf == "list" else "0")
     n = 1 << 18
     umem, desc = D.synth_umem(n, L, stride, faulty=True, peaked=True, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=payloadsz, flags=D.F_CSUM)
     res, cnt, table, launches = run_bench_form(umem, desc, cfg)
-    assert launches.get("rx_fixup", 0) == 1, launches
+    assert fused_ran(launches, 1) and launches.get("rx_fixup", 0) == (1 if ovf == "list" else 0), launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     assert_same(res, cnt, table, ores, ocnt, otable)
 
@@ -180,7 +196,7 @@ def test_slice_pass_over_a_full_stage_of_batches():
         k = q.histogram_batches_per_pass()
     assert k == 32
     res, cnt, table, launches = run_bench_form(umem, desc, cfg, batches=k)
-    assert launches.get("rx_fixup", 0) == k and launches.get("rx_slice_histo", 0) == 1, launches
+    assert fused_ran(launches, k) and launches.get("rx_slice_histo", 0) == 1, launches
     ores, ocnt, otable = oracle_full(umem, desc, cfg)
     otable *= k
     ocnt = {kk: (v if kk == "first_abort_idx" else k * v) for kk, v in ocnt.items()}

@@ -138,13 +138,13 @@ FUSED_CASES = [c for c in CASES if c[4] != D.MODE_WAVEFORM and not (c[5] & D.F_N
 def test_fused_decode_parity(L, stride, faulty, payloadsz, mode, flags):
     """Partitioned batches without a record buffer and per-packet accounting
     take rx_decode_fused (keys bucketed in LDS, appended to per-XCD segments,
-    checksum-failed frames taken back by rx_fixup); batch-abort falls back to
+    checksum-failed frames taken back by the decode); batch-abort falls back to
     the records path.  Results, counters and the whole table vs the oracle."""
     umem, desc = D.synth_umem(6000, L, stride, faulty=faulty)
     cfg = D.RxConfig(payloadsz=payloadsz, mode=mode, flags=flags | D.F_HISTO_PARTITIONED)
     ores, ocnt = compare(umem, desc, cfg, check_hist=True, records=False)
     if faulty and flags & D.F_CSUM:
-        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 0  # the fixup has frames to take back
+        assert (ores["status"] == D.RX_INVALID_UDP_CSUM).sum() > 0  # the decode has frames to take back
 
 
 @pytest.mark.parametrize("records", [True, False], ids=["records", "fused"])
