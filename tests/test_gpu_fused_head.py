@@ -183,3 +183,23 @@ def test_frame_maps_vs_oracle(policy, fmap, monkeypatch):
     cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_PARTITIONED)
     ores, ocnt = compare(umem, desc, cfg, check_hist=True, records=False)
     assert ocnt["first_abort_idx"] < len(desc)
+
+
+@pytest.mark.parametrize("flags", [D.F_CSUM, D.F_CSUM | D.F_CSUM_WRITEBACK, D.F_CSUM | D.F_PREFILTER],
+                         ids=["csum", "writeback", "prefilter"])
+@pytest.mark.parametrize("seed", [31, 47])
+def test_decode_only_edge_frames_vs_oracle(flags, seed):
+    """Decode-only batches (no histogram, no record buffer: BASELINE
+    configs[1]'s form; the records-path decode streams every datagram for its
+    checksum and decodes no event) on the edge frames above -- any byte
+    offset, IP options, datagrams ending inside the first line, odd lengths,
+    bad and absent checksums, first lines past the UMEM end: every result,
+    every counter (and with writeback, every UMEM byte) equals the oracle's.
+    (r06k: a first-line hand-off variant of this decode passed these too, and
+    was slower.)"""
+    _need_gpu()
+    umem, desc = frames(seed)
+    cfg = D.RxConfig(payloadsz=1458, flags=flags | D.F_NO_HISTO, port_start=0, port_end=65535)
+    ores, ocnt = compare(umem, desc, cfg, check_hist=False, records=False)
+    st = ores["status"]
+    assert (st == D.RX_OK).sum() > 1000 and (st == D.RX_INVALID_UDP_CSUM).sum() > 50, np.unique(st, return_counts=True)
