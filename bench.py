@@ -317,8 +317,16 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     runs = items * 129 * 2  # u16 slice-run offsets per item
     touched = 0
     if histo and E:
-        kk = d_keys[:K]
-        touched = int(torch.unique(kk[kk >= 0] >> 14).numel())  # 16K-bin slices with >= 1 event
+        # 16K-bin slices with >= 1 event: a scatter of flags in 64M-key chunks
+        # (torch.unique's sort of 586M keys at 9000 B ran for minutes with two
+        # ranks sharing a GPU, r06m)
+        occ = torch.zeros(1 << 16, dtype=torch.uint8, device=dev)
+        for c0 in range(0, K, 1 << 26):
+            s = d_keys[c0:min(K, c0 + (1 << 26))]
+            occ[(s[s >= 0] >> 14).long()] = 1
+            del s
+        touched = int(occ.sum().item())
+        del occ
     alg = {
         # the metric's path: desc + frame (the UDP checksum reads all of it) + result + 4-B record per event
         # (the fused decode writes 8-B key triples, 2.67 B per event, so this over-counts
@@ -720,6 +728,9 @@ def run_e2e(args, torch, dist, dev, rank, world, local):
 
 def main():
     args = parse_args()
+    if os.environ.get("DQDK_BENCH_WATCHDOG"):  # (diagnostics: every rank's stack on stderr every N s)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DQDK_BENCH_WATCHDOG"]), repeat=True)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))  # before any HIP call in this process
