@@ -110,6 +110,72 @@ struct Reg {
     void* dev;
 };
 
+// Host UMEM registrations, process-wide and reference-counted: HIP keeps one
+// registration per host range, not one per caller, so several queues over
+// one UMEM (DQDK's workers share it: src/dqdk.c) share one registration and
+// the last of them to let go unregisters it.  (Before round 6 every queue
+// registered and unregistered the range itself: the first queue's destroy
+// took the mapping from under the others -- found when destroy began
+// reporting the failed hipHostUnregister of the second queue.)
+struct GReg {
+    void* host;
+    uint64_t size;
+    void* dev;
+    int refs;
+};
+std::mutex g_reg_mu;
+std::vector<GReg> g_regs;
+
+// one reference to the registration of [host, host + size): an existing one
+// at least that large, or a new one (a smaller one held by nobody else is
+// replaced; one held by other queues cannot grow under them: -EBUSY)
+int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, bool* own_kept)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    *own_kept = replacing_own;  // (the caller's reference survives a failure unless released below)
+    for (size_t k = 0; k < g_regs.size(); k++) {
+        GReg& g = g_regs[k];
+        if (g.host != host)
+            continue;
+        if (g.size >= size) {
+            if (!replacing_own)
+                g.refs++;
+            *dev_out = g.dev;
+            return 0;
+        }
+        if (g.refs > (replacing_own ? 1 : 0))
+            return fail_errno(-EBUSY, "umem_register: a larger UMEM at an address other queues hold registered");
+        *own_kept = false;
+        g_regs.erase(g_regs.begin() + (long)k);
+        HIPCHK(hipHostUnregister(host));
+        break;
+    }
+    HIPCHK(hipHostRegister(host, size, hipHostRegisterMapped | hipHostRegisterPortable));
+    void* dev = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dev, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return fail("hipHostGetDevicePointer", e);
+    }
+    g_regs.push_back({host, size, dev, 1});
+    *dev_out = dev;
+    return 0;
+}
+
+// drop one reference; the last one unregisters
+hipError_t greg_release(void* host)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (size_t k = 0; k < g_regs.size(); k++)
+        if (g_regs[k].host == host) {
+            if (--g_regs[k].refs > 0)
+                return hipSuccess;
+            g_regs.erase(g_regs.begin() + (long)k);
+            return hipHostUnregister(host);
+        }
+    return hipErrorHostMemoryNotRegistered;
+}
+
 // Device memory: plain (hipMalloc) or physically contiguous
 // (hipDeviceMallocContiguous).  UMEM images from dqdk_gpu_device_alloc are
 // contiguous (DQDK_GPU_IMAGE_ALLOC=plain: plain); the queue's table and
@@ -1343,7 +1409,7 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     if (q->raw_stream)
         chk(hipStreamSynchronize(q->raw_stream), "hipStreamSynchronize(raw stream)");  // no D2H into h_rawb may outlive it
     for (auto& r : q->regs)
-        chk(hipHostUnregister(r.host), "hipHostUnregister(umem)");
+        chk(greg_release(r.host), "hipHostUnregister(umem)");
     for (auto& p : q->pending) {
         chk(hipEventDestroy(p.a), "hipEventDestroy(timing)");
         chk(hipEventDestroy(p.b), "hipEventDestroy(timing)");
@@ -1469,25 +1535,26 @@ int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size)
     if (!q || !umem || !size)
         return -EINVAL;
     SETDEV(q->device);
+    bool own = false;
     for (size_t k = 0; k < q->regs.size(); k++) {
         if (q->regs[k].host != umem)
             continue;
         if (q->regs[k].size >= size)
             return 0;
         // the same address with more bytes (a larger buffer in the old one's
-        // place, or a grown view): the old registration is replaced, never
-        // reused past its end
+        // place, or a grown view): the registration is replaced, never
+        // reused past its end (this queue's work on it drained first)
         HIPCHK(hipStreamSynchronize(q->stream));
-        HIPCHK(hipHostUnregister(umem));
         q->regs.erase(q->regs.begin() + (long)k);
+        own = true;
         break;
     }
-    HIPCHK(hipHostRegister(umem, size, hipHostRegisterMapped));
     void* dev = nullptr;
-    hipError_t e = hipHostGetDevicePointer(&dev, umem, 0);
-    if (e != hipSuccess) {
-        (void)hipHostUnregister(umem);
-        return fail("hipHostGetDevicePointer", e);
+    bool kept = false;
+    if (int rc = greg_acquire(umem, size, own, &dev, &kept)) {
+        if (kept)  // (the smaller registration this queue held: still its reference, released later)
+            q->regs.push_back({umem, 0, nullptr});
+        return rc;
     }
     q->regs.push_back({umem, size, dev});
     return 0;
@@ -1501,8 +1568,8 @@ int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem)
         if (q->regs[k].host == umem) {
             SETDEV(q->device);
             HIPCHK(hipStreamSynchronize(q->stream));
-            HIPCHK(hipHostUnregister(umem));
             q->regs.erase(q->regs.begin() + (long)k);
+            HIPCHK(greg_release(umem));
             return 0;
         }
     }

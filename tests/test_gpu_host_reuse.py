@@ -117,3 +117,35 @@ def test_destroy_reports_success_and_device_free_checks():
     buf = D.DeviceBuffer(0, 1 << 20)
     buf.close()
     buf.close()  # no-op
+
+
+@pytest.mark.parametrize("close_first", [0, 1])
+def test_queues_sharing_one_umem_keep_their_mapping(close_first):
+    """DQDK's workers share one UMEM (a queue each): every queue registers it,
+    HIP keeps ONE registration per host range.  The library counts the
+    queues holding it, so closing one queue leaves the others' zero-copy
+    mapping in place (before round 6 the first destroy unregistered the range
+    from under the others, and their own destroy then failed).  Three queues
+    over one host UMEM: batches on each, one closed, the others run another
+    batch each (results and counters vs the oracle), all close cleanly."""
+    _need_gpu()
+    n = 2048
+    umem, desc = D.synth_umem(2 * n, 1500, 4096, faulty=True)
+    d0, d1 = desc[:n].copy(), desc[n:].copy()
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_ATOMIC)
+    qs = [D.RxQueue(0, cfg, n) for _ in range(3)]
+    try:
+        for q in qs:
+            res, _ = q.process_batch(umem, d0)
+        qs[close_first].close()  # raises if its teardown failed
+        ores, ocnt, _ = O.rx_batch(umem.copy(), d1, cfg.payloadsz, cfg.mode, cfg.flags)
+        for k, q in enumerate(qs):
+            if k == close_first:
+                continue
+            res, delta = q.process_batch(umem, d1)
+            np.testing.assert_array_equal(res, ores)
+            assert delta["rcvd_pkts"] == ocnt["rcvd_pkts"] and delta["total_events"] == ocnt["total_events"]
+        torch.cuda.synchronize()
+    finally:
+        for q in qs:
+            q.close()
