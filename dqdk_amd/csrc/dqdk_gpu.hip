@@ -108,6 +108,7 @@ struct Reg {
     void* host;
     uint64_t size;
     void* dev;
+    void* base;  // the process-wide registration it holds a reference to (GReg::host)
 };
 
 // Host UMEM registrations, process-wide and reference-counted: HIP keeps one
@@ -129,10 +130,22 @@ std::vector<GReg> g_regs;
 // one reference to the registration of [host, host + size): an existing one
 // at least that large, or a new one (a smaller one held by nobody else is
 // replaced; one held by other queues cannot grow under them: -EBUSY)
-int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, bool* own_kept)
+int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, bool* own_kept, void** base_out)
 {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     *own_kept = replacing_own;  // (the caller's reference survives a failure unless released below)
+    *base_out = host;
+    if (!replacing_own) {
+        // inside another queue's registration (a view of a shared UMEM)
+        const uint8_t* h = (const uint8_t*)host;
+        for (GReg& g : g_regs)
+            if (g.host != host && (const uint8_t*)g.host <= h && h + size <= (const uint8_t*)g.host + g.size) {
+                g.refs++;
+                *dev_out = (uint8_t*)g.dev + (h - (const uint8_t*)g.host);
+                *base_out = g.host;
+                return 0;
+            }
+    }
     for (size_t k = 0; k < g_regs.size(); k++) {
         GReg& g = g_regs[k];
         if (g.host != host)
@@ -1409,7 +1422,7 @@ int dqdk_gpu_queue_destroy(dqdk_gpu_queue_t* q)
     if (q->raw_stream)
         chk(hipStreamSynchronize(q->raw_stream), "hipStreamSynchronize(raw stream)");  // no D2H into h_rawb may outlive it
     for (auto& r : q->regs)
-        chk(greg_release(r.host), "hipHostUnregister(umem)");
+        chk(greg_release(r.base), "hipHostUnregister(umem)");
     for (auto& p : q->pending) {
         chk(hipEventDestroy(p.a), "hipEventDestroy(timing)");
         chk(hipEventDestroy(p.b), "hipEventDestroy(timing)");
@@ -1545,18 +1558,23 @@ int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size)
         // place, or a grown view): the registration is replaced, never
         // reused past its end (this queue's work on it drained first)
         HIPCHK(hipStreamSynchronize(q->stream));
+        void* const old_base = q->regs[k].base;
         q->regs.erase(q->regs.begin() + (long)k);
-        own = true;
+        if (old_base != umem)  // (it was a view inside another registration: that reference goes)
+            HIPCHK(greg_release(old_base));
+        else
+            own = true;
         break;
     }
     void* dev = nullptr;
+    void* base = umem;
     bool kept = false;
-    if (int rc = greg_acquire(umem, size, own, &dev, &kept)) {
+    if (int rc = greg_acquire(umem, size, own, &dev, &kept, &base)) {
         if (kept)  // (the smaller registration this queue held: still its reference, released later)
-            q->regs.push_back({umem, 0, nullptr});
+            q->regs.push_back({umem, 0, nullptr, umem});
         return rc;
     }
-    q->regs.push_back({umem, size, dev});
+    q->regs.push_back({umem, size, dev, base});
     return 0;
 }
 
@@ -1568,8 +1586,9 @@ int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem)
         if (q->regs[k].host == umem) {
             SETDEV(q->device);
             HIPCHK(hipStreamSynchronize(q->stream));
+            void* const base = q->regs[k].base;
             q->regs.erase(q->regs.begin() + (long)k);
-            HIPCHK(greg_release(umem));
+            HIPCHK(greg_release(base));
             return 0;
         }
     }

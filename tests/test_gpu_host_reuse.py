@@ -149,3 +149,31 @@ def test_queues_sharing_one_umem_keep_their_mapping(close_first):
     finally:
         for q in qs:
             q.close()
+
+
+def test_view_inside_another_queues_umem_shares_its_registration():
+    """A queue handed a view INSIDE a UMEM another queue registered (an
+    interior address: HIP refuses a second, overlapping registration) shares
+    that registration at the view's offset, and keeps it after the first
+    queue closes: its batches before and after equal the oracle's."""
+    _need_gpu()
+    n = 1024
+    umem, desc = D.synth_umem(2 * n, 1500, 4096, faulty=True)
+    cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM | D.F_HISTO_ATOMIC)
+    off = n * 4096  # the view starts at frame n
+    view = umem[off:]
+    dv = desc[n:].copy()
+    dv["addr"] -= off
+    ores, ocnt, _ = O.rx_batch(view.copy(), dv, cfg.payloadsz, cfg.mode, cfg.flags)
+    qa, qb = D.RxQueue(0, cfg, 2 * n), D.RxQueue(0, cfg, n)
+    try:
+        qa.process_batch(umem, desc)
+        res, delta = qb.process_batch(view, dv)
+        np.testing.assert_array_equal(res, ores)
+        qa.close()
+        res, delta = qb.process_batch(view, dv)
+        np.testing.assert_array_equal(res, ores)
+        assert delta["rcvd_pkts"] == ocnt["rcvd_pkts"]
+    finally:
+        qa.close()
+        qb.close()
