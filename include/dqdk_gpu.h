@@ -202,7 +202,12 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
  * BEFORE its memory is freed or unmapped: a registration outlives nothing it
  * maps, and a new buffer placed at a freed one's address would otherwise be
  * read through the old registration's pages (the reference's UMEM lives
- * for the worker's lifetime, src/dqdk.c:109-127, so this is its order too). */
+ * for the worker's lifetime, src/dqdk.c:109-127, so this is its order too).
+ * Registrations are process-wide and reference-counted: queues (on any GPU)
+ * over one UMEM, as DQDK's workers share theirs, or over views inside it,
+ * share one mapping, and the last queue to unregister or be destroyed
+ * releases it.  Replacing a registration another queue still holds fails
+ * with -EBUSY. */
 int dqdk_gpu_umem_register(dqdk_gpu_queue_t* q, void* umem, uint64_t size);
 int dqdk_gpu_umem_unregister(dqdk_gpu_queue_t* q, void* umem);
 int dqdk_gpu_rx_batch(dqdk_gpu_queue_t* q, const uint8_t* umem, uint64_t umem_size, const dqdk_gpu_desc_t* d,
