@@ -121,7 +121,6 @@ struct Reg {
 struct GReg {
     void* host;
     uint64_t size;
-    void* dev;
     int refs;
 };
 std::mutex g_reg_mu;
@@ -135,13 +134,18 @@ int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, 
     std::lock_guard<std::mutex> lk(g_reg_mu);
     *own_kept = replacing_own;  // (the caller's reference survives a failure unless released below)
     *base_out = host;
+    // (a shared registration's device address is asked for on the caller's
+    // device: queues over one UMEM may sit on different GPUs)
+    auto dev_of = [](void* h, void** d) { return hipHostGetDevicePointer(d, h, 0); };
     if (!replacing_own) {
         // inside another queue's registration (a view of a shared UMEM)
         const uint8_t* h = (const uint8_t*)host;
         for (GReg& g : g_regs)
             if (g.host != host && (const uint8_t*)g.host <= h && h + size <= (const uint8_t*)g.host + g.size) {
+                void* d = nullptr;
+                HIPCHK(dev_of(g.host, &d));
                 g.refs++;
-                *dev_out = (uint8_t*)g.dev + (h - (const uint8_t*)g.host);
+                *dev_out = (uint8_t*)d + (h - (const uint8_t*)g.host);
                 *base_out = g.host;
                 return 0;
             }
@@ -151,9 +155,11 @@ int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, 
         if (g.host != host)
             continue;
         if (g.size >= size) {
+            void* d = nullptr;
+            HIPCHK(dev_of(host, &d));
             if (!replacing_own)
                 g.refs++;
-            *dev_out = g.dev;
+            *dev_out = d;
             return 0;
         }
         if (g.refs > (replacing_own ? 1 : 0))
@@ -165,12 +171,12 @@ int greg_acquire(void* host, uint64_t size, bool replacing_own, void** dev_out, 
     }
     HIPCHK(hipHostRegister(host, size, hipHostRegisterMapped | hipHostRegisterPortable));
     void* dev = nullptr;
-    const hipError_t e = hipHostGetDevicePointer(&dev, host, 0);
+    const hipError_t e = dev_of(host, &dev);
     if (e != hipSuccess) {
         (void)hipHostUnregister(host);
         return fail("hipHostGetDevicePointer", e);
     }
-    g_regs.push_back({host, size, dev, 1});
+    g_regs.push_back({host, size, 1});
     *dev_out = dev;
     return 0;
 }
