@@ -165,7 +165,10 @@ __device__ __forceinline__ uint32_t staged_range_sum(const uint32_t (&w)[32], in
 // kHeadA: it also decodes the events and sums the checksum bytes of the
 // frame's first cache line (frame_geo's a_end) into akey[0, na) / fi.head.
 // ---------------------------------------------------------------------------
-template <bool kHeadA>
+// kHalf: the frame's second 64 B are read only when its headers reach them
+// (the records-path tiles: rx_decode, rx_small; r06r: configs[1]'s decode
+// -2 %, the fused decode unchanged, so it keeps one 128-B read)
+template <bool kHeadA, bool kHalf>
 __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameInfo& fi, dqdk_gpu_rx_result_t& r,
                                             bool& needB, uint32_t (&akey)[kAEv], uint32_t& na, uint32_t& hw, bool& sh)
 {
@@ -181,17 +184,34 @@ __device__ __forceinline__ void parse_frame(const RxArgs& a, uint32_t i, FrameIn
     // 8 aligned chunks = 128 B from a0: covers frame bytes [0, 113) for any off0
     // (the headers need [0, 97)).
     uint32_t w[32];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
+    auto ld = [&](int k, bool on) {
         u32x4 v = {0u, 0u, 0u, 0u};
         uint64_t o = a0 + 16ull * k;
-        if (addr < a.umem_size && o + 16 <= a.umem_size)
+        if (on && addr < a.umem_size && o + 16 <= a.umem_size)
             v = *(const u32x4*)(a.umem + o);
         w[4 * k + 0] = v.x;
         w[4 * k + 1] = v.y;
         w[4 * k + 2] = v.z;
         w[4 * k + 3] = v.w;
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        ld(k, true);
+    // The second 64 B only where the parse reads them: without kHeadA it
+    // reads a0-relative bytes below off0 + 22 + 4 ihl (prefilter fields,
+    // IPv4 header, UDP header, the head correction's bytes before it), so a
+    // frame whose headers end inside the first 64 B leaves those bytes 0
+    // (ihl = FB(14) & 15: byte 2 of frame dword 3, from w[3..7])
+    bool more = true;
+    if (kHalf && !kHeadA) {
+        const uint32_t q0 = off0 >> 2, rb0 = off0 & 3;
+        const uint32_t d3 = __builtin_amdgcn_alignbyte(sel4(w[4], w[5], w[6], w[7], q0),
+                                                       sel4(w[3], w[4], w[5], w[6], q0), rb0);
+        more = off0 + 22u + 4u * ((d3 >> 16) & 15u) > 64u;
     }
+#pragma unroll
+    for (int k = 4; k < 8; k++)
+        ld(k, more);
     // h[m] = frame dword m (frame-relative, unaligned-safe): static indices below.
     const uint32_t q = off0 >> 2, rb = off0 & 3;
     uint32_t s[22], h[21];
@@ -671,7 +691,7 @@ __device__ __forceinline__ void process_window(const RxArgs& a, const PFrame& P,
 }
 
 // ---- phase A: lane parses frame i and prepares its stream (shared by both decodes) ----
-template <bool kHeadA = false>
+template <bool kHeadA = false, bool kHalf = false>
 __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, FrameInfo& fi,
                                         dqdk_gpu_rx_result_t& r, LaneFrame& lf, bool& stream,
                                         uint32_t (&akey)[kAEv], uint32_t& na, uint32_t& hw)
@@ -683,7 +703,7 @@ __device__ __forceinline__ void phase_a(const RxArgs& a, uint32_t i, bool live, 
     for (int k = 0; k < kAEv; k++)
         akey[k] = DQDK_KEY_NONE;
     if (live)
-        parse_frame<kHeadA>(a, i, fi, r, needB, akey, na, hw, sh);
+        parse_frame<kHeadA, kHalf>(a, i, fi, r, needB, akey, na, hw, sh);
     stream = false;
     lf.base_lo = lf.base_hi = lf.nrec = lf.pk1 = 0;
     lf.pk2 = kNoWin | (kNoWin << 11);
@@ -896,7 +916,7 @@ __device__ __forceinline__ void decode_wave_tile(const RxArgs& a, uint32_t tile,
     LaneFrame lf;
     bool stream;
     uint32_t akey[kAEv], na, hw;
-    phase_a(a, i, live, fi, r, lf, stream, akey, na, hw);
+    phase_a<false, true>(a, i, live, fi, r, lf, stream, akey, na, hw);
 
     // ---- phase B: stream the frames ----
     const uint64_t smask0 = __ballot(stream);
