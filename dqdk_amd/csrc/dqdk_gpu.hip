@@ -113,8 +113,9 @@ struct Reg {
 
 // Host UMEM registrations, process-wide and reference-counted: HIP keeps one
 // registration per host range, not one per caller, so several queues over
-// one UMEM (DQDK's workers share it: src/dqdk.c) share one registration and
-// the last of them to let go unregisters it.  (Before round 6 every queue
+// one host buffer (a caller may hand one UMEM to several workers' queues --
+// the reference allocates one per worker, src/dqdk.c:562 -- or views inside
+// one) share one registration and the last of them to let go unregisters it.  (Before round 6 every queue
 // registered and unregistered the range itself: the first queue's destroy
 // took the mapping from under the others -- found when destroy began
 // reporting the failed hipHostUnregister of the second queue.)

@@ -204,7 +204,8 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
  * read through the old registration's pages (the reference's UMEM lives
  * for the worker's lifetime, src/dqdk.c:109-127, so this is its order too).
  * Registrations are process-wide and reference-counted: queues (on any GPU)
- * over one UMEM, as DQDK's workers share theirs, or over views inside it,
+ * over one host buffer (the reference gives each worker its own UMEM,
+ * src/dqdk.c:562, but a caller may share one) or over views inside it
  * share one mapping, and the last queue to unregister or be destroyed
  * releases it.  Replacing a registration another queue still holds fails
  * with -EBUSY. */

@@ -121,8 +121,10 @@ def test_destroy_reports_success_and_device_free_checks():
 
 @pytest.mark.parametrize("close_first", [0, 1])
 def test_queues_sharing_one_umem_keep_their_mapping(close_first):
-    """DQDK's workers share one UMEM (a queue each): every queue registers it,
-    HIP keeps ONE registration per host range.  The library counts the
+    """Several queues over one host UMEM (the drop-in harness's workers read
+    one mlock'ed image, tests/c/fetch_xsk_harness.c; the reference gives each
+    worker its own, src/dqdk.c:562): every queue registers it, but HIP keeps
+    ONE registration per host range.  The library counts the
     queues holding it, so closing one queue leaves the others' zero-copy
     mapping in place (before round 6 the first destroy unregistered the range
     from under the others, and their own destroy then failed).  Three queues

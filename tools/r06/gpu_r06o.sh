@@ -1,6 +1,6 @@
 #!/bin/bash
 # r06o: host UMEM registrations reference-counted across queues (several
-# workers over one UMEM): the -m gpu suite once (new shared-UMEM test), then
+# queues over one host buffer, as the latency harness's workers): the -m gpu suite once (new shared-UMEM test), then
 # the drop-in latency sweep with 1 and 3 workers (r06n's 3-worker run failed
 # at teardown: the second queue's hipHostUnregister found no registration).
 set -e
