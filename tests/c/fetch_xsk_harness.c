@@ -4,8 +4,11 @@
  * pieces DQDK wraps around the receive loop modelled in plain C (libxdp is
  * not in this image):
  *
- *   UMEM       mmap(MAP_HUGETLB when available, src/dqdk-mem.c:12-28) +
- *              mlock, the frames of an input image copied in
+ *   UMEM       one per worker, as umem_info_create makes it for each
+ *              (src/dqdk.c:562, :57-72): mmap(MAP_HUGETLB when available,
+ *              src/dqdk-mem.c:12-28) + mlock, the frames of an input image
+ *              copied in (DQDK_HARNESS_SHARED_UMEM=1: one UMEM for every
+ *              worker's queue, a layout the library also serves)
  *   RX ring    power-of-two descriptor ring with producer / consumer
  *              indices and a cached consumer (xsk_ring_cons__peek advances
  *              it, __release publishes it); a producer ("the NIC") refills
@@ -257,6 +260,22 @@ static void* read_file(const char* path, size_t* len)
     return p;
 }
 
+/* a UMEM: hugepage mapping when the host has them, else 4-KiB pages; mlock'ed */
+static uint8_t* map_umem(size_t size, const uint8_t* image, size_t len, int* hugetlb, int* locked)
+{
+    *hugetlb = 1;
+    uint8_t* u = mmap(NULL, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_HUGETLB, -1, 0);
+    if (u == MAP_FAILED) {
+        *hugetlb = 0;
+        u = mmap(NULL, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    }
+    if (u == MAP_FAILED)
+        return NULL;
+    *locked = mlock(u, size) == 0;
+    memcpy(u, image, len);
+    return u;
+}
+
 static int cmp_u64(const void* a, const void* b)
 {
     const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
@@ -308,23 +327,25 @@ int main(int argc, char** argv)
     }
     const uint32_t ndesc = (uint32_t)(desc_len / sizeof(dqdk_gpu_desc_t));
 
-    /* UMEM: hugepage mapping when the host has them, else 4-KiB pages; mlock'ed */
+    /* UMEMs: one per worker (src/dqdk.c:562), or one shared */
     const size_t huge = 2u << 20;
     const size_t size = (umem_len + huge - 1) / huge * huge;
-    int hugetlb = 1;
-    uint8_t* umem = mmap(NULL, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_HUGETLB, -1, 0);
-    if (umem == MAP_FAILED) {
-        hugetlb = 0;
-        umem = mmap(NULL, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    const char* sh = getenv("DQDK_HARNESS_SHARED_UMEM");
+    const int shared = sh && atoi(sh) != 0;
+    const int numem = shared ? 1 : nworkers;
+    uint8_t** umems = calloc((size_t)numem, sizeof(uint8_t*));
+    int hugetlb = 1, locked = 1;
+    for (int k = 0; k < numem; k++) {
+        int h = 0, l = 0;
+        if (!(umems[k] = map_umem(size, image, umem_len, &h, &l))) {
+            perror("mmap");
+            return 1;
+        }
+        hugetlb &= h;
+        locked &= l;
     }
-    if (umem == MAP_FAILED) {
-        perror("mmap");
-        return 1;
-    }
-    const int locked = mlock(umem, size) == 0;
-    memcpy(umem, image, umem_len);
     free(image);
-    printf("umem_hugetlb %d\numem_mlocked %d\n", hugetlb, locked);
+    printf("umem_hugetlb %d\numem_mlocked %d\numem_count %d\n", hugetlb, locked, numem);
 
     dqdk_gpu_cfg_t cfg = { .payloadsz = (uint32_t)atoi(argv[7]), .mode = (uint32_t)atoi(argv[8]),
                            .flags = (uint32_t)strtoul(argv[9], NULL, 0) };
@@ -341,6 +362,7 @@ int main(int argc, char** argv)
     const uint64_t total = (uint64_t)ndesc * repeat;
     for (int k = 0; k < nworkers; k++) {
         dqdk_worker_t* x = &w[k];
+        uint8_t* const umem = umems[shared ? 0 : k];
         x->index = k;
         x->umem = umem;
         x->umem_len = umem_len;
@@ -483,13 +505,16 @@ int main(int argc, char** argv)
     for (int k = 0; k < nworkers; k++) {
         if (!fp) {
             /* a UMEM is unregistered before it is freed (include/dqdk_gpu.h) */
-            if (dqdk_gpu_umem_unregister(w[k].q, umem) || dqdk_gpu_queue_destroy(w[k].q)) {
+            if (dqdk_gpu_umem_unregister(w[k].q, w[k].umem) || dqdk_gpu_queue_destroy(w[k].q)) {
                 fprintf(stderr, "teardown: %s\n", dqdk_gpu_last_error());
                 bad = 1;
             }
         }
     }
-    munlock(umem, size);
-    munmap(umem, size);
+    for (int k = 0; k < numem; k++) {
+        munlock(umems[k], size);
+        munmap(umems[k], size);
+    }
+    free(umems);
     return bad;
 }

@@ -1,7 +1,7 @@
 """Per-call latency and rate of the two drop-in forms at DQDK's batch sizes.
 
 Runs build/fetch_xsk_harness (tests/c/) over synthetic frames in mlock'ed host
-UMEM, for
+UMEM (one per worker, as src/dqdk.c:562 allocates them), for
   proc = batch  INTEGRATION.md's fetch_xsk patch (dqdk_gpu_rx_batch, UMEM
                 registered once: the GPU reads the frames over PCIe)
   proc = fp     the unpatched fetch_xsk / process_frame / get_udp_payload with
@@ -44,7 +44,7 @@ def run(proc: str, batch: int, workers: int, flen: int, psz: int, frames: int, n
     loop_s = out["loop_ns"] / 1e9
     done_s = (out["loop_ns"] + out["fini_ns"]) / 1e9
     return {
-        "proc": proc, "batch": batch, "workers": workers, "frame_len": flen, "payloadsz": psz,
+        "proc": proc, "batch": batch, "workers": workers, "umems": out["umem_count"], "frame_len": flen, "payloadsz": psz,
         "slot_payloads": slot if proc == "fp" else None,
         "frames": out["rcvd_frames"], "events": out["total_events"],
         "mpkts_loop": out["rcvd_frames"] / loop_s / 1e6,
