@@ -202,7 +202,9 @@ int dqdk_gpu_queue_sync(dqdk_gpu_queue_t* q);
  * BEFORE its memory is freed or unmapped: a registration outlives nothing it
  * maps, and a new buffer placed at a freed one's address would otherwise be
  * read through the old registration's pages (the reference's UMEM lives
- * for the worker's lifetime, src/dqdk.c:109-127, so this is its order too).
+ * for the worker's lifetime: created at src/dqdk.c:562, unmapped by
+ * umem_info_free at :476-479 (:74-80) in the worker's cleanup, so this is its
+ * order too).
  * Registrations are process-wide and reference-counted: queues (on any GPU)
  * over one host buffer (the reference gives each worker its own UMEM,
  * src/dqdk.c:562, but a caller may share one) or over views inside it

@@ -15,7 +15,8 @@ same, a larger and a smaller second buffer, with and without the pageable
 copy before the registration, and with the registration dropped by
 unregister or by the queue's destroy.  The ownership rule it rests on is the
 reference's: frames are valid until the descriptors are released
-(src/dqdk.c:300) and the UMEM lives as long as its worker (src/dqdk.c:109-127).
+(src/dqdk.c:300) and the UMEM lives as long as its worker (src/dqdk.c:562,
+freed at :476-479).
 """
 import ctypes as C
 
