@@ -11,7 +11,9 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 d=gpurun_out/pmc_${tag}_$L
 mkdir -p $d
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD"; do
+# (pass 4: read requests by size -- 4 TCC counters, the block's limit)
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" \
+           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $grp -d $d/p$i -o run --output-format csv -- \
         python3 bench.py --frame-len $L --frames ${FRAMES:-1048576} --steps 3 --warmup 1 --no-cpu-baseline --no-9000 "$@" > $d/p$i.log 2>&1

@@ -1,7 +1,12 @@
 """Summarise rocprofv3 PMC passes (tools/pmc.sh) per kernel: mean per dispatch.
 
-FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 reports half the
-bytes of wide coalesced reads); FETCH_SIZE / WRITE_SIZE are in KB.
+Read bytes: with the request-size pass (TCC_EA0_RDREQ_{32B,64B,128B}_sum),
+exactly 32 / 64 / 128 B per request of each size (`hbm_read_bytes_by_size`,
+used as `hbm_read_bytes_corrected`); FETCH_SIZE's own expression counts
+128-B requests through TCC_BUBBLE, which on gfx950 misses them, so it is
+also kept doubled as MI355X_MICROARCH.md prescribes for wide coalesced
+reads (`hbm_read_bytes_fetch_x2`) -- a doubling that overcounts 64-B
+requests (r06w).  FETCH_SIZE / WRITE_SIZE are in KB.
 
 usage: python tools/pmc_summary.py <pmc dir> [<summary.json> <workload key>]
 The workload key is the one bench.py looks up: "<frame_len>:<csum|nocsum>:<frames>".
@@ -38,7 +43,14 @@ def summarise(d: Path) -> dict:
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         m["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in m:
-            m["hbm_read_bytes_corrected"] = m["FETCH_SIZE"] * 1024 * 2
+            m["hbm_read_bytes_fetch_x2"] = m["FETCH_SIZE"] * 1024 * 2
+            m["hbm_read_bytes_corrected"] = m["hbm_read_bytes_fetch_x2"]
+        sz = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+        if all(c in m for c in sz):
+            m["hbm_read_bytes_by_size"] = 32 * m[sz[0]] + 64 * m[sz[1]] + 128 * m[sz[2]]
+            if "TCC_EA0_RDREQ_sum" in m:  # requests of none of the three sizes (expected 0)
+                m["rdreq_unsized"] = m["TCC_EA0_RDREQ_sum"] - m[sz[0]] - m[sz[1]] - m[sz[2]]
+            m["hbm_read_bytes_corrected"] = m["hbm_read_bytes_by_size"]
         if "WRITE_SIZE" in m:
             m["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
