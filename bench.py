@@ -396,17 +396,27 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     # the fused decode ran: rx_part2 without the records path's rx_part1 (the
     # fused path launches rx_part1, as "rx_fixup", only to group a long overflow list)
     fused = st.get("rx_part2", {}).get("launches", 0) > 0 and not st.get("rx_part1", {}).get("launches", 0)
-    traffic = None
+    traffic = traffic_x2 = None
+    traffic_src = None
     try:
         pmc = json.loads(Path(args.pmc).read_text())
         w = pmc.get(f"{L}:{'csum' if not args.no_csum else 'nocsum'}:{n}", {})
-        traffic = w.get("rx_decode_fused_kernel" if fused else "rx_decode_kernel", {}).get("hbm_bytes_per_launch")
+        kd = w.get("rx_decode_fused_kernel" if fused else "rx_decode_kernel", {})
+        traffic = kd.get("hbm_bytes_per_launch")
+        if traffic is not None:
+            # reads from the request-size counters when collected (tools/pmc_summary.py),
+            # else FETCH_SIZE x 2; the doubled figure kept beside the exact one
+            exact = "hbm_read_bytes_by_size" in kd
+            traffic_src = ("TCC_EA0_RDREQ_{32B,64B,128B} + WRITE_SIZE" if exact else "FETCH_SIZE x 2 + WRITE_SIZE")
+            if exact and "hbm_read_bytes_fetch_x2" in kd:
+                traffic_x2 = kd["hbm_read_bytes_fetch_x2"] + kd.get("hbm_write_bytes", 0.0)
     except Exception:
         pass
     dec = st.get("rx_decode", {})
     roofline = {"bound": "hbm", "kernel": "rx_decode_fused" if fused else "rx_decode",
                 "achieved": dec.get("GB_s"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": dec.get("frac_hbm"), "traffic": traffic,
+                "frac": dec.get("frac_hbm"), "traffic": traffic, "traffic_counters": traffic_src,
+                "traffic_fetch_x2": traffic_x2,
                 "alg_bytes_per_frame": round(16 + Lm + 8 + (4 * E if keys_written else 0), 1),
                 "frames_per_launch": n,
                 # the decode launches bracketed by HIP events inside the timed region (of args.steps)
