@@ -2,7 +2,7 @@
 profiles/pmc_summary.json), so its byte arithmetic is checked on synthetic
 rocprofv3 counter CSVs: FETCH_SIZE doubled, WRITE_SIZE in KB, and -- with the
 request-size pass -- read bytes as 32 / 64 / 128 B per request, which then
-replace the doubled FETCH_SIZE (a doubling that overcounts 64-B requests)."""
+replace the doubled FETCH_SIZE (exact for any request mix)."""
 import csv
 import importlib.util
 from pathlib import Path

@@ -5,8 +5,10 @@ exactly 32 / 64 / 128 B per request of each size (`hbm_read_bytes_by_size`,
 used as `hbm_read_bytes_corrected`); FETCH_SIZE's own expression counts
 128-B requests through TCC_BUBBLE, which on gfx950 misses them, so it is
 also kept doubled as MI355X_MICROARCH.md prescribes for wide coalesced
-reads (`hbm_read_bytes_fetch_x2`) -- a doubling that overcounts 64-B
-requests (r06w).  FETCH_SIZE / WRITE_SIZE are in KB.
+reads (`hbm_read_bytes_fetch_x2`).  The two agree within 0.1 % for this
+path's kernels, whose reads leave L2 as 128-B requests (r06w); the exact
+form also holds where requests are 32 or 64 B.  FETCH_SIZE / WRITE_SIZE are
+in KB.
 
 usage: python tools/pmc_summary.py <pmc dir> [<summary.json> <workload key>]
 The workload key is the one bench.py looks up: "<frame_len>:<csum|nocsum>:<frames>".
