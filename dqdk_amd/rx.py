@@ -263,9 +263,9 @@ class RxQueue:
         buffer (-1: undecided or off) and each candidate's best decode ns per
         frame (include/dqdk_gpu.h)."""
         ch = C.c_int(-1)
-        ns = (C.c_float * 8)()
-        k = L.check(L.lib().dqdk_gpu_queue_staging_probe(self._h, C.byref(ch), ns, 8), "staging_probe")
-        return {"chosen": ch.value, "ns_per_frame": [round(ns[i], 4) for i in range(k)]}
+        ns = (C.c_float * 16)()
+        k = L.check(L.lib().dqdk_gpu_queue_staging_probe(self._h, C.byref(ch), ns, 16), "staging_probe")
+        return {"chosen": ch.value, "ns_per_frame": [round(ns[i], 4) for i in range(min(k, 16))]}
 
     # -- stage timing --------------------------------------------------------
     def enable_timing(self, on: bool = True) -> None:

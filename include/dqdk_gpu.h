@@ -420,7 +420,7 @@ const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
  * *chosen = the kept candidate (-1: not decided yet or off), ns_per_frame[k]
  * = candidate k's best decode time per frame (0: untimed), k < ncand.
  * Returns the number of candidates. */
-#define DQDK_GPU_PROBE_CANDS 5
+#define DQDK_GPU_PROBE_CANDS 8  /* (5 until round 6: one fast placement in five was common at 9000 B) */
 int dqdk_gpu_queue_staging_probe(dqdk_gpu_queue_t* q, int* chosen, float* ns_per_frame, int ncand);
 
 const char* dqdk_gpu_last_error(void);
