@@ -8,7 +8,9 @@ proc=batch, INTEGRATION.md's fetch_xsk patch (dqdk_gpu_rx_batch):
     GPU counters equal the reference's recorded F4 counters and the CSV equals
     the reference's table (tests/golden/gen_tristan.py);
   * 31 batches of 100 over the stream repeated three times (batch abort on):
-    equal to the oracle (pinned to F4) applied batch by batch.
+    equal to the oracle (pinned to F4) applied batch by batch;
+  * three workers over a UMEM each (the reference's layout) or one shared
+    UMEM: three times the oracle's counters, every teardown clean.
 
 proc=fp, the reference's plugin API: fetch_xsk / process_frame /
 get_udp_payload unpatched, dqdk_gpu_frame_processor registered as the
@@ -43,19 +45,19 @@ STATS = ["rcvd_frames", "rcvd_pkts", "rcvd_bytes", "invalid_ip_pkts", "invalid_u
 
 
 def run_harness(tmp_path, umem, desc, batch, ring, start, repeat, psz, mode, flags, proc="batch", workers=1,
-                slot=0):
+                slot=0, want_csv=True, env=None):
     _need_gpu()
     assert HARNESS.exists(), "build/fetch_xsk_harness not built (python -m dqdk_amd._build)"
     (tmp_path / "umem.bin").write_bytes(np.ascontiguousarray(umem).tobytes())
     (tmp_path / "desc.bin").write_bytes(np.ascontiguousarray(desc).tobytes())
     csv = tmp_path / "histo.csv"
     p = subprocess.run([str(HARNESS), str(tmp_path / "umem.bin"), str(tmp_path / "desc.bin"), str(batch), str(ring),
-                        str(start), str(repeat), str(psz), str(mode), str(flags), str(csv), proc, str(workers),
-                        str(slot)],
-                       capture_output=True, text=True, timeout=120)
-    assert p.returncode == 0, p.stderr
+                        str(start), str(repeat), str(psz), str(mode), str(flags), str(csv) if want_csv else "-", proc,
+                        str(workers), str(slot)],
+                       capture_output=True, text=True, timeout=120, env=dict(os.environ, **(env or {})))
+    assert p.returncode == 0, p.stderr  # (teardown included: every queue's unregister and destroy)
     out = dict(l.split() for l in p.stdout.splitlines() if l.strip())
-    return {k: int(v) for k, v in out.items()}, csv.read_text()
+    return {k: int(v) for k, v in out.items()}, csv.read_text() if want_csv else None
 
 
 @pytest.mark.parametrize("csum", [0, 1])
@@ -97,6 +99,33 @@ def test_many_batches_over_wrapping_ring(tmp_path):
     nz = np.flatnonzero(table)
     assert got["histo_nonzero"] == len(nz)
     assert csv == ref_csv(nz.astype(np.uint32), table[nz].astype(np.uint64))
+
+
+@pytest.mark.parametrize("shared", [0, 1])
+def test_three_workers_batch_patch_either_umem_layout(tmp_path, shared):
+    """Three workers, a queue each, every one running the whole descriptor
+    stream: over a UMEM each (as umem_info_create makes one per worker,
+    src/dqdk.c:562) or over one shared UMEM (DQDK_HARNESS_SHARED_UMEM=1: the
+    library's reference-counted registration, include/dqdk_gpu.h).  Worker
+    stats and GPU counters are three times the oracle's, and every queue's
+    unregister and destroy succeed."""
+    z = np.load(GOLD / "f4_batch.npz")
+    mode, psz = (int(x) for x in z["cfg"])
+    flags = D.F_CSUM | D.F_BATCH_ABORT
+    batch, repeat = 100, 2
+    got, _ = run_harness(tmp_path, z["umem"], z["desc"], batch=batch, ring=256, start=200, repeat=repeat, psz=psz,
+                         mode=mode, flags=flags, workers=3, want_csv=False,
+                         env={"DQDK_HARNESS_SHARED_UMEM": str(shared)})
+    assert got["workers"] == 3 and got["umem_count"] == (1 if shared else 3)
+    stream = np.concatenate([z["desc"]] * repeat)
+    tot = dict.fromkeys(STATS, 0)
+    umem = z["umem"].copy()
+    for b0 in range(0, len(stream), batch):
+        _, c, _ = O.rx_batch(umem, stream[b0:b0 + batch], psz, mode, flags, want_keys=False)
+        for k in STATS:
+            tot[k] += c[k]
+    for k in STATS:
+        assert got[k] == 3 * tot[k], (k, got[k], 3 * tot[k])
 
 
 # ---- the plugin API: dqdk_gpu_frame_processor behind the unpatched loop ----
