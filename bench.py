@@ -231,11 +231,11 @@ def measure(args, L, torch, dist, dev, rank, world, local, cpu_sec, image=None):
     for _ in range(args.warmup):
         step()
     # the queue's staging placement probe (include/dqdk_gpu.h: its first
-    # 2 x DQDK_GPU_PROBE_CANDS fused batches try candidate piece buffers, the
+    # 3 x DQDK_GPU_PROBE_CANDS fused batches try candidate piece buffers, the
     # next keeps the fastest) belongs to the warmup: extra untimed batches
     # until it has decided
     warm_extra = 0
-    while q.staging_probe()["chosen"] < 0 and warm_extra < 32 and n >= 65536 and histo and E and \
+    while q.staging_probe()["chosen"] == -1 and warm_extra < 32 and n >= 65536 and histo and E and \
             not pass_records:
         step()
         warm_extra += 1

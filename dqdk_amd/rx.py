@@ -260,7 +260,7 @@ class RxQueue:
 
     def staging_probe(self) -> dict:
         """The staging placement probe's outcome: the kept candidate piece
-        buffer (-1: undecided or off) and each candidate's best decode ns per
+        buffer (-1: undecided, -2: off) and each candidate's best decode ns per
         frame (include/dqdk_gpu.h)."""
         ch = C.c_int(-1)
         ns = (C.c_float * 16)()

@@ -413,12 +413,13 @@ const char* dqdk_gpu_timing_stage_name(int stage); /* NULL when out of range */
 /* The fused decode's rate depends on where its piece buffer lands physically
  * relative to the UMEM image it reads.  A queue's first
  * fused batches of at least 65536 frames run on DQDK_GPU_PROBE_CANDS candidate
- * piece buffers in turn (each candidate's first batch untimed, then one more
- * batch each, its decode timed by HIP events: 2 x DQDK_GPU_PROBE_CANDS
- * batches); at the next such batch the fastest is kept, the others freed
- * (DQDK_GPU_STAGING_PROBE=0 at queue creation: off).  This reads the outcome:
- * *chosen = the kept candidate (-1: not decided yet or off), ns_per_frame[k]
- * = candidate k's best decode time per frame (0: untimed), k < ncand.
+ * piece buffers in turn (each candidate's first batch untimed, then two more
+ * batches each, in order and then in reverse order, their decodes timed by
+ * HIP events: 3 x DQDK_GPU_PROBE_CANDS batches); at the next such batch the
+ * fastest mean is kept, the others freed (DQDK_GPU_STAGING_PROBE=0 at queue
+ * creation: off).  This reads the outcome: *chosen = the kept candidate (-1:
+ * not decided yet, -2: off), ns_per_frame[k] = candidate k's mean decode
+ * time per frame (0: untimed), k < ncand.
  * Returns the number of candidates. */
 #define DQDK_GPU_PROBE_CANDS 8  /* (5 until round 6: one fast placement in five was common at 9000 B) */
 int dqdk_gpu_queue_staging_probe(dqdk_gpu_queue_t* q, int* chosen, float* ns_per_frame, int ncand);

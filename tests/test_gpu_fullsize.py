@@ -203,15 +203,17 @@ def test_slice_pass_over_a_full_stage_of_batches():
     assert_same(res, cnt, table, ores, ocnt, otable)
 
 
-def test_staging_probe_switches_piece_buffers_exactly():
+def test_staging_probe_switches_piece_buffers_exactly(monkeypatch):
     """The staging placement probe (include/dqdk_gpu.h): a queue's first
-    2 x DQDK_GPU_PROBE_CANDS fused batches of >= 64K frames run on the
-    candidate piece buffers in turn (the decode's pieces and its overflow
+    3 x DQDK_GPU_PROBE_CANDS fused batches of >= 64K frames run on the
+    candidate piece buffers (untimed, then timed in order and in reverse
+    order; the decode's pieces and its overflow
     regions live there), the next on the fastest, the others freed.  Faulty,
     peaked frames (pieces and overflow regions both used) over three batches
     more than the probe takes: the table, results and counters are k times
-    the oracle's, and the probe has decided."""
+    the oracle's, and the probe has decided (on by default)."""
     _need_gpu()
+    monkeypatch.delenv("DQDK_GPU_STAGING_PROBE", raising=False)
     n = 1 << 16
     umem, desc = D.synth_umem(n, 1500, 4096, faulty=True, peaked=True, threads=HOST_THREADS)
     cfg = D.RxConfig(payloadsz=1458, flags=D.F_CSUM)
@@ -221,7 +223,7 @@ def test_staging_probe_switches_piece_buffers_exactly():
     d_res = torch.full((n * 8,), 0xEE, dtype=torch.uint8, device=dev)
     with D.RxQueue(0, cfg, n) as q:
         ncand = len(q.staging_probe()["ns_per_frame"])
-        k = 2 * ncand + 3
+        k = 3 * ncand + 3
         q.set_stream(torch.cuda.current_stream().cuda_stream)
         for b in range(k):
             q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), None)
@@ -241,11 +243,15 @@ def test_staging_probe_switches_piece_buffers_exactly():
 
 
 def test_staging_probe_off_and_below_its_batch_size(monkeypatch):
-    """DQDK_GPU_STAGING_PROBE=0 at queue creation, or batches under 64K
-    frames: no probe (chosen stays -1, nothing timed)."""
+    """DQDK_GPU_STAGING_PROBE=0 at queue creation (chosen -2), or batches
+    under 64K frames (on, unset or =1, but never started: -1): nothing
+    timed."""
     _need_gpu()
-    for env, n in (("0", 1 << 16), ("1", 4096)):
-        monkeypatch.setenv("DQDK_GPU_STAGING_PROBE", env)
+    for env, n, want in (("0", 1 << 16, -2), (None, 4096, -1), ("1", 4096, -1)):
+        if env is None:
+            monkeypatch.delenv("DQDK_GPU_STAGING_PROBE", raising=False)
+        else:
+            monkeypatch.setenv("DQDK_GPU_STAGING_PROBE", env)
         umem, desc = D.synth_umem(n, 1500, 4096, threads=HOST_THREADS)
         dev = torch.device("cuda:0")
         d_umem = torch.from_numpy(umem).to(dev)
@@ -257,4 +263,4 @@ def test_staging_probe_off_and_below_its_batch_size(monkeypatch):
                 q.process_device(d_umem.data_ptr(), umem.nbytes, d_desc.data_ptr(), n, d_res.data_ptr(), None)
             torch.cuda.synchronize()
             p = q.staging_probe()
-        assert p["chosen"] == -1 and not any(p["ns_per_frame"]), (env, n, p)
+        assert p["chosen"] == want and not any(p["ns_per_frame"]), (env, n, p)
